@@ -1,0 +1,153 @@
+/*
+ * pow_gpu.h — C ABI of the MI355X (gfx950) proof-of-work miner.
+ *
+ * Drop-in for the mining hot path of MPI_blockchain (reference at
+ * /root/reference): the inner loop of proof_of_work (node.cpp:292-308),
+ *     gen_random_nonce (block.cpp:61-72)
+ *  -> block_to_hash    (block.cpp:74-88, picosha2::hash256_hex_string)
+ *  -> solves_problem   (block.cpp:91-96)
+ * moves behind these entry points.  Everything else (node.cpp's MPI protocol,
+ * the success tail node.cpp:311-327) stays host C/C++.
+ *
+ * The reference has no FFI for this path; its de-facto boundary is the
+ * free-function set declared in block.h:27-30 and called from the pthread
+ * entry `void* proof_of_work(void*)` (node.h:15).  Each entry point below says
+ * which of those it replaces.
+ *
+ * Conventions
+ *   - Plain C: pointers and sizes only, no exceptions across the ABI.
+ *   - Return codes: >= 0 success (meaning per function), < 0 error, one of
+ *     POW_E* below (HIP failures are reported as POW_EHIP; pow_last_error()
+ *     gives the text).
+ *   - A pow_ctx is bound to one GPU and is NOT thread-safe: exactly one
+ *     thread (that rank's mining thread) drives it.  The only cross-thread
+ *     input is the cancel word passed to pow_mine, which any thread may bump.
+ *   - The caller owns every pow_block and output array; the library owns the
+ *     device buffers, the HIP stream and the per-template constants.
+ *
+ * Counter nonces.  The reference draws 9 chars with rand()%62 (block.cpp:61-72).
+ * The GPU path replaces the RNG by a deterministic counter: counter c maps to
+ * the 9 base-62 digits of c, most significant first, through the reference's
+ * alphabet (0-25 -> 'a'..'z', 26-51 -> 'A'..'Z', 52-61 -> '0'..'9'), followed
+ * by NUL.  The counter space is [0, 62^9).  Any nonce the reference can draw
+ * is reachable, with the same probability of solving per trial.
+ */
+#ifndef POW_GPU_H
+#define POW_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define POW_HASH_SIZE 256  /* block.h:4 HASH_SIZE  */
+#define POW_NONCE_SIZE 10  /* block.h:5 NONCE_SIZE */
+#define POW_MSG_BYTES 270  /* 4 header bytes + nonce[10] + prev[256] (block.cpp:79-88) */
+#define POW_COUNTER_LIMIT 13537086546263552ULL /* 62^9 */
+
+/* Byte-identical to the reference's `struct Block` (block.h:17-25) on LP64:
+ * sizeof 552; offsets index 0, node_owner_number 4, difficulty 8,
+ * created_at 16, nonce 24, previous_block_hash 34, block_hash 290.
+ * A reference Block* may be passed wherever a pow_block* is expected. */
+typedef struct pow_block {
+  uint32_t index;
+  uint32_t node_owner_number;
+  uint32_t difficulty;
+  uint64_t created_at; /* `unsigned long int` in block.h:21 */
+  char nonce[POW_NONCE_SIZE];
+  char previous_block_hash[POW_HASH_SIZE];
+  char block_hash[POW_HASH_SIZE];
+} pow_block;
+
+typedef struct pow_ctx pow_ctx;
+
+enum {
+  POW_OK = 0,
+  POW_EINVAL = -1,    /* bad argument (null pointer, range past 62^9, d > 256, ...) */
+  POW_ENOSPC = -2,    /* pow_sweep: more solutions than `cap` */
+  POW_EHIP = -3,      /* a HIP runtime call failed; see pow_last_error() */
+  POW_ENODEV = -4,    /* no such GPU */
+};
+
+/* Per-call statistics of the last pow_mine / pow_sweep / pow_hash_blocks. */
+typedef struct pow_stats {
+  double kernel_ms;      /* sum of HIP-event-timed kernel durations on the ctx stream */
+  uint32_t launches;     /* kernels launched by the call */
+  uint64_t hashes;       /* trials issued to the GPU (incl. edge lanes masked out) */
+} pow_stats;
+
+/* ---- context --------------------------------------------------------- */
+int pow_init(int device, pow_ctx** out);
+void pow_destroy(pow_ctx* ctx);
+const char* pow_last_error(void);
+int pow_get_stats(const pow_ctx* ctx, pow_stats* out);
+/* Device properties the roofline uses: CU count and peak engine clock (kHz). */
+int pow_device_info(const pow_ctx* ctx, int* cu_count, int* clock_khz, char* name, size_t name_cap);
+
+/* ---- host helpers (no GPU work) ---------------------------------------- */
+/* Counter -> nonce[10] (9 base-62 chars MSB first + NUL).
+ * Replaces gen_random_nonce (block.cpp:61-72) with a deterministic mapping.
+ * Returns POW_EINVAL if ctr >= 62^9. */
+int pow_nonce_from_counter(uint64_t ctr, char nonce[POW_NONCE_SIZE]);
+/* Exact 270-byte message the reference hashes (block_to_str, block.cpp:79-88):
+ * low byte of index, owner, difficulty, created_at; nonce[0..9]; prev[0..255]. */
+int pow_block_to_bytes(const pow_block* b, uint8_t out[POW_MSG_BYTES]);
+/* solves_problem (block.cpp:91-96) with a run-time difficulty: the first
+ * `diff_bits` binary digits of the 64-char hex digest are all '0'. */
+int pow_solves_problem(const char* hex, unsigned diff_bits);
+
+/* ---- GPU entry points -------------------------------------------------- */
+/* block_to_hash (block.cpp:74-77) for a batch of blocks on the GPU.
+ * digests: n*32 bytes (may be NULL); hex: n*65 chars, 64 lowercase hex + NUL
+ * each (may be NULL).  Returns POW_OK. */
+int pow_hash_blocks(pow_ctx* ctx, const pow_block* blocks, size_t n,
+                    uint8_t* digests, char* hex);
+/* Single-block convenience form of the above. */
+int pow_hash_block(pow_ctx* ctx, const pow_block* b, uint8_t digest[32], char hex[65]);
+
+/* Mining round: replaces node.cpp:302-308 (nonce -> hash -> test) for every
+ * counter in [ctr_start, ctr_start + ctr_count).  The header fields and the
+ * 256-byte previous_block_hash are taken from `tmpl` as they are (the caller
+ * does the template refresh of node.cpp:292-299).
+ *   diff_bits     leading zero BITS required (T3), 0..256.
+ *   cancel_word   optional; polled between GPU sub-rounds; if it differs from
+ *                 `epoch` the call stops early and returns 0.
+ * On success returns 1 and fills *out = *tmpl with out->nonce = the nonce of
+ * the LOWEST solving counter in range and out->block_hash = its 64-char hex
+ * digest + NUL (strcpy semantics of node.cpp:318: bytes 65..255 keep tmpl's);
+ * *found_ctr = that counter.  Returns 0 if the range holds no solution or the
+ * call was cancelled.  *hashes_done (optional) = trials issued. */
+int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+             unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+             pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
+
+/* Deterministic parity / throughput mode: every solving counter of
+ * [ctr_start, ctr_start + ctr_count) (ctr_count <= 2^32), written to out_ctrs
+ * as (counter - ctr_start), ascending.  *n_found = number of solutions
+ * (also when it exceeds cap, in which case POW_ENOSPC is returned and the
+ * first `cap` entries are an unspecified subset).  out_ctrs may be NULL when
+ * cap == 0 (count only).  Returns POW_OK. */
+int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+              unsigned diff_bits, uint32_t* out_ctrs, size_t cap, size_t* n_found);
+
+/* Sweep variant that leaves the (unsorted) solution list on the device and
+ * returns only the count and the lowest solving counter (UINT64_MAX if none):
+ * the shape a sharded multi-GPU round needs (the 8-byte min goes to an RCCL
+ * all-reduce).  dev_out may be NULL (count + min only). */
+int pow_sweep_device(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                     unsigned diff_bits, uint32_t* dev_out, size_t cap, size_t* n_found,
+                     uint64_t* min_ctr);
+
+/* Device memory on the ctx's GPU (for pow_sweep_device's dev_out). */
+int pow_dev_alloc(pow_ctx* ctx, size_t bytes, void** out);
+int pow_dev_free(pow_ctx* ctx, void* p);
+/* Copy `bytes` from a device pointer to host memory (synchronous). */
+int pow_dev_read(pow_ctx* ctx, const void* dev, void* host, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POW_GPU_H */

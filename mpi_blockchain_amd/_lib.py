@@ -1,0 +1,116 @@
+"""ctypes binding of ``libpow_gpu.so`` (include/pow_gpu.h, include/pow_tools.h).
+
+There is deliberately NO fallback: if the native library is missing or fails
+to load, this raises.  The product path never routes through a CPU
+implementation (the CPU checkers live in ``oracle/`` and are test-only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libpow_gpu.so")
+
+HASH_SIZE = 256
+NONCE_SIZE = 10
+MSG_BYTES = 270
+COUNTER_LIMIT = 62**9
+
+POW_OK, POW_EINVAL, POW_ENOSPC, POW_EHIP, POW_ENODEV = 0, -1, -2, -3, -4
+_ERRNAMES = {POW_EINVAL: "POW_EINVAL", POW_ENOSPC: "POW_ENOSPC", POW_EHIP: "POW_EHIP",
+             POW_ENODEV: "POW_ENODEV"}
+
+
+class PowError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Block(ctypes.Structure):
+    """``struct Block`` of block.h:17-25 (== ``pow_block``), sizeof 552."""
+
+    _fields_ = [
+        ("index", ctypes.c_uint32),
+        ("node_owner_number", ctypes.c_uint32),
+        ("difficulty", ctypes.c_uint32),
+        ("created_at", ctypes.c_uint64),
+        ("nonce", ctypes.c_char * NONCE_SIZE),
+        ("previous_block_hash", ctypes.c_char * HASH_SIZE),
+        ("block_hash", ctypes.c_char * HASH_SIZE),
+    ]
+
+
+class PowStats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("launches", ctypes.c_uint32),
+                ("hashes", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(Block) == 552
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libpow_gpu.so (raises if it is missing — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -m mpi_blockchain_amd.build` "
+            "(the GPU path has no CPU fallback)")
+    # One HIP runtime per process: when PyTorch-ROCm is importable, load it
+    # first so this library binds to the same libamdhip64.so.7 (same soname).
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the C ABI
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER(Block)
+    c_u64p = ctypes.POINTER(ctypes.c_uint64)
+    c_sizep = ctypes.POINTER(ctypes.c_size_t)
+    sigs = {
+        "pow_init": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "pow_destroy": ([ctypes.c_void_p], None),
+        "pow_last_error": ([], ctypes.c_char_p),
+        "pow_get_stats": ([ctypes.c_void_p, ctypes.POINTER(PowStats)], ctypes.c_int),
+        "pow_device_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                             ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        "pow_nonce_from_counter": ([ctypes.c_uint64, ctypes.c_char_p], ctypes.c_int),
+        "pow_block_to_bytes": ([P, ctypes.c_char_p], ctypes.c_int),
+        "pow_solves_problem": ([ctypes.c_char_p, ctypes.c_uint], ctypes.c_int),
+        "pow_hash_blocks": ([ctypes.c_void_p, P, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p],
+                            ctypes.c_int),
+        "pow_hash_block": ([ctypes.c_void_p, P, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        "pow_mine": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                      ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
+        "pow_sweep": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, c_sizep], ctypes.c_int),
+        "pow_sweep_device": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                              ctypes.c_void_p, ctypes.c_size_t, c_sizep, c_u64p], ctypes.c_int),
+        "pow_dev_alloc": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "pow_dev_free": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+        "pow_dev_read": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+        "pow_valu_peak": ([ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
+                          ctypes.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+EXPORTS = ("pow_init", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
+           "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
+           "pow_hash_block", "pow_mine", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
+           "pow_dev_read", "pow_valu_peak")
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise PowError(rc, (load().pow_last_error() or b"").decode(errors="replace"))
+    return rc

@@ -1,0 +1,519 @@
+// C ABI of the gfx950 miner (include/pow_gpu.h): context, per-template
+// precompute, launch sizing, result read-back.
+//
+// Replaces the inner loop of proof_of_work (node.cpp:292-308) and
+// block_to_hash (block.cpp:74-77); see include/pow_gpu.h for the mapping of
+// each entry point to the reference function it replaces.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pow_gpu.h"
+#include "pow_template.h"
+
+static_assert(sizeof(pow_block) == 552, "pow_block must match block.h:17-25 (LP64)");
+static_assert(offsetof(pow_block, created_at) == 16, "layout");
+static_assert(offsetof(pow_block, nonce) == 24, "layout");
+static_assert(offsetof(pow_block, previous_block_hash) == 34, "layout");
+static_assert(offsetof(pow_block, block_hash) == 290, "layout");
+static_assert(sizeof(PowConsts) % 4 == 0 && sizeof(PowConsts) < 4096, "consts");
+
+hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
+                             const PowLaunch& L, uint32_t* out, PowResult* res);
+hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(POW_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                               \
+  } while (0)
+
+// ---------------- host SHA-256 pieces for the template precompute ----------------
+// (FIPS 180-4 / picosha2.h:46-136; only the parts needed to fold constants)
+const uint32_t kK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+const uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                         0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+inline uint32_t ssig0(uint32_t x) { return rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3); }
+inline uint32_t ssig1(uint32_t x) { return rotr(x, 17) ^ rotr(x, 19) ^ (x >> 10); }
+inline uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// block.cpp:61-72 alphabet.
+inline char digit_char(unsigned d) {
+  return d < 26 ? (char)('a' + d) : d < 52 ? (char)('A' + d - 26) : (char)('0' + d - 52);
+}
+
+// block.cpp:79-88 + picosha2.h:201-218: the padded 320-byte message.
+void padded_message(const pow_block* b, uint8_t m[320]) {
+  memset(m, 0, 320);
+  pow_block_to_bytes(b, m);
+  m[POW_MSG_BYTES] = 0x80;
+  const uint64_t bits = (uint64_t)POW_MSG_BYTES * 8;  // 2160
+  for (int i = 0; i < 8; ++i) m[319 - i] = (uint8_t)(bits >> (8 * i));
+}
+
+void expand(uint32_t w[64], const uint8_t* chunk) {
+  for (int i = 0; i < 16; ++i) w[i] = be32(chunk + 4 * i);
+  for (int i = 16; i < 64; ++i) w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+}
+
+}  // namespace
+
+void pow_build_consts(const pow_block* tmpl, PowConsts* C) {
+  memset(C, 0, sizeof *C);
+  pow_block b = *tmpl;
+  memset(b.nonce, 0, sizeof b.nonce);  // nonce bytes are per trial; nonce[9] stays NUL
+  uint8_t m[320];
+  padded_message(&b, m);
+  for (int c = 1; c < 5; ++c) {
+    uint32_t w[64];
+    expand(w, m + 64 * c);
+    for (int i = 0; i < 64; ++i) C->kw[c - 1][i] = kK[i] + w[i];
+  }
+  uint32_t W[16];
+  for (int i = 0; i < 16; ++i) W[i] = be32(m + 4 * i);
+  C->w0 = W[0];
+  C->w3lo = W[3] & 0x00FFFFFFu;  // [nonce[9]=0, prev[0], prev[1]]
+  for (int i = 4; i < 16; ++i) C->kw0[i] = kK[i] + W[i];
+  // round 0 of chunk 0 (uniform)
+  uint32_t a = kIV[0], bb = kIV[1], c = kIV[2], d = kIV[3], e = kIV[4], f = kIV[5], g = kIV[6], h = kIV[7];
+  {
+    uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    uint32_t chv = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + chv + kK[0] + W[0];
+    uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    uint32_t mj = (a & bb) ^ (a & c) ^ (bb & c);
+    h = g; g = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + S0 + mj;
+  }
+  const uint32_t st[8] = {a, bb, c, d, e, f, g, h};
+  memcpy(C->st0, st, sizeof st);
+  C->u16 = ssig1(W[14]) + W[9] + W[0];
+  C->u17 = ssig1(W[15]) + W[10];
+  C->u19 = W[12] + ssig0(W[4]);
+  C->u20 = W[13] + ssig0(W[5]) + W[4];
+  C->u21 = W[14] + ssig0(W[6]) + W[5];
+  C->u22 = W[15] + ssig0(W[7]) + W[6];
+  C->u23 = ssig0(W[8]) + W[7];
+  C->u24 = ssig0(W[9]) + W[8];
+  for (int k = 0; k < 6; ++k) C->u25[k] = ssig0(W[10 + k]) + W[9 + k];
+  C->w15 = W[15];
+  for (unsigned j = 0; j < POW_J; ++j) {
+    const uint32_t w3 = ((uint32_t)(uint8_t)digit_char(j) << 24) | C->w3lo;
+    C->w3[j] = w3;
+    C->kw3[j] = kK[3] + w3;
+    C->u18[j] = ssig0(w3) + W[11];
+  }
+}
+
+struct pow_ctx {
+  int device = 0;
+  int cu_count = 0;
+  int clock_khz = 0;
+  char name[256] = {0};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  PowConsts* d_consts = nullptr;
+  PowResult* d_res = nullptr;
+  PowResult* h_res = nullptr;  // pinned
+  uint32_t* d_out = nullptr;
+  size_t out_cap = 0;
+  uint32_t* d_msgs = nullptr;
+  uint32_t* d_dig = nullptr;
+  size_t hash_cap = 0;
+  unsigned grid_full = 0;  // workgroups that fill the chip (8 per CU)
+  bool force_full = false; // POW_FORCE_FULL=1: use the d > 32 kernel for every d (tests)
+  pow_stats stats{};
+};
+
+namespace {
+
+int set_dev(const pow_ctx* ctx) {
+  HIP_OK(hipSetDevice(ctx->device));
+  return POW_OK;
+}
+
+// Split [start, start+count) (count <= 2^32) into the kernel's prefix form.
+int make_launch(uint64_t start, uint64_t count, unsigned diff, uint32_t cap, uint32_t mode,
+                PowLaunch* L) {
+  memset(L, 0, sizeof *L);
+  const uint64_t P0 = start / POW_J;
+  L->off0 = (uint32_t)(start - P0 * POW_J);
+  const uint64_t np = (L->off0 + count + POW_J - 1) / POW_J;
+  if (np > 0xFFFFFFFFull - (1u << 26)) return fail(POW_EINVAL, "launch too large");
+  L->n_prefix = (uint32_t)np;
+  uint64_t p = P0;
+  for (int i = 7; i >= 0; --i) {
+    L->base_digit[i] = (uint32_t)(p % 62);
+    p /= 62;
+  }
+  L->count = count;
+  L->diff = diff;
+  L->thr = diff >= 32 ? 0u : (0xFFFFFFFFu >> diff);
+  L->cap = cap;
+  L->mode = mode;
+  return POW_OK;
+}
+
+unsigned grid_for(const pow_ctx* ctx, uint32_t n_prefix) {
+  const uint64_t want = ((uint64_t)n_prefix + 255) / 256;
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, ctx->grid_full));
+}
+
+int check_range(const pow_block* tmpl, uint64_t start, uint64_t count, unsigned diff) {
+  if (!tmpl) return fail(POW_EINVAL, "null template");
+  if (diff > 256) return fail(POW_EINVAL, "difficulty %u > 256 bits", diff);
+  if (start >= POW_COUNTER_LIMIT || count > POW_COUNTER_LIMIT - start)
+    return fail(POW_EINVAL, "counter range past 62^9");
+  return POW_OK;
+}
+
+// One timed launch of K1 over [start, start+count) (count <= 2^32) with the
+// consts already resident; leaves the result in ctx->h_res.
+int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint32_t mode,
+               uint32_t* dev_out, uint32_t cap) {
+  PowLaunch L;
+  int rc = make_launch(start, count, diff, cap, mode, &L);
+  if (rc) return rc;
+  PowResult init{};
+  init.min_rel = ~0ull;
+  HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+  const unsigned grid = grid_for(ctx, L.n_prefix);
+  HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIP_OK(pow_launch_search((int)mode, diff > 32 || ctx->force_full, grid, ctx->stream, ctx->d_consts, L, dev_out,
+                           ctx->d_res));
+  HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
+  HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->stats.kernel_ms += ms;
+  ctx->stats.launches += 1;
+  ctx->stats.hashes += mode == 1 ? ctx->h_res->hashes : (uint64_t)L.n_prefix * POW_J;
+  return POW_OK;
+}
+
+int upload_consts(pow_ctx* ctx, const pow_block* tmpl) {
+  PowConsts C;
+  pow_build_consts(tmpl, &C);
+  HIP_OK(hipMemcpyAsync(ctx->d_consts, &C, sizeof C, hipMemcpyHostToDevice, ctx->stream));
+  return POW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pow_last_error(void) { return g_err.c_str(); }
+
+int pow_init(int device, pow_ctx** out) {
+  if (!out) return fail(POW_EINVAL, "null out");
+  *out = nullptr;
+  int n = 0;
+  HIP_OK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(POW_ENODEV, "device %d of %d", device, n);
+  HIP_OK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(POW_ENODEV, "device %d is %s; this library is built for gfx950 only", device,
+                prop.gcnArchName);
+  pow_ctx* ctx = new pow_ctx;
+  ctx->device = device;
+  ctx->cu_count = prop.multiProcessorCount;
+  ctx->clock_khz = prop.clockRate;
+  snprintf(ctx->name, sizeof ctx->name, "%s", prop.name);
+  ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u;  // 8 x 256-thread WGs = 32 waves/CU
+  if (const char* ff = getenv("POW_FORCE_FULL")) ctx->force_full = ff[0] == '1';
+  if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
+    const int per = atoi(g);
+    if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
+  }
+  int rc = POW_OK;
+  auto chk = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && rc == POW_OK) rc = fail(POW_EHIP, "%s: %s", what, hipGetErrorString(e));
+  };
+  chk(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
+  chk(hipEventCreate(&ctx->ev0), "hipEventCreate");
+  chk(hipEventCreate(&ctx->ev1), "hipEventCreate");
+  chk(hipMalloc(&ctx->d_consts, sizeof(PowConsts)), "hipMalloc consts");
+  chk(hipMalloc(&ctx->d_res, sizeof(PowResult)), "hipMalloc result");
+  chk(hipHostMalloc(&ctx->h_res, sizeof(PowResult), hipHostMallocDefault), "hipHostMalloc");
+  if (rc != POW_OK) {
+    pow_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return POW_OK;
+}
+
+void pow_destroy(pow_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(ctx->d_consts);
+  (void)hipFree(ctx->d_res);
+  (void)hipFree(ctx->d_out);
+  (void)hipFree(ctx->d_msgs);
+  (void)hipFree(ctx->d_dig);
+  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int pow_get_stats(const pow_ctx* ctx, pow_stats* out) {
+  if (!ctx || !out) return fail(POW_EINVAL, "null");
+  *out = ctx->stats;
+  return POW_OK;
+}
+
+int pow_device_info(const pow_ctx* ctx, int* cu_count, int* clock_khz, char* name, size_t name_cap) {
+  if (!ctx) return fail(POW_EINVAL, "null");
+  if (cu_count) *cu_count = ctx->cu_count;
+  if (clock_khz) *clock_khz = ctx->clock_khz;
+  if (name && name_cap) snprintf(name, name_cap, "%s", ctx->name);
+  return POW_OK;
+}
+
+int pow_nonce_from_counter(uint64_t ctr, char nonce[POW_NONCE_SIZE]) {
+  if (!nonce) return fail(POW_EINVAL, "null nonce");
+  if (ctr >= POW_COUNTER_LIMIT) return fail(POW_EINVAL, "counter >= 62^9");
+  for (int i = POW_NONCE_SIZE - 2; i >= 0; --i) {
+    nonce[i] = digit_char((unsigned)(ctr % 62));
+    ctr /= 62;
+  }
+  nonce[POW_NONCE_SIZE - 1] = 0;  // block.cpp:71
+  return POW_OK;
+}
+
+int pow_block_to_bytes(const pow_block* b, uint8_t out[POW_MSG_BYTES]) {
+  if (!b || !out) return fail(POW_EINVAL, "null");
+  // block.cpp:81-84: std::string::operator+=(char) keeps the low byte (trap T1)
+  out[0] = (uint8_t)b->index;
+  out[1] = (uint8_t)b->node_owner_number;
+  out[2] = (uint8_t)b->difficulty;
+  out[3] = (uint8_t)b->created_at;
+  memcpy(out + 4, b->nonce, POW_NONCE_SIZE);                        // block.cpp:85
+  memcpy(out + 4 + POW_NONCE_SIZE, b->previous_block_hash, POW_HASH_SIZE);  // block.cpp:86
+  return POW_OK;
+}
+
+int pow_solves_problem(const char* hex, unsigned diff_bits) {
+  if (!hex) return 0;
+  // block.cpp:28-58, 91-96: binary expansion of the hex string (toupper;
+  // non-hex chars count as "1111"), first diff_bits chars must be '0'.
+  const size_t len = strlen(hex);
+  if ((size_t)diff_bits > 4 * len) return 0;
+  for (unsigned i = 0; i < diff_bits; ++i) {
+    char c = hex[i / 4];
+    unsigned v;
+    if (c >= '0' && c <= '9') v = (unsigned)(c - '0');
+    else if ((c >= 'a' && c <= 'e') || (c >= 'A' && c <= 'E')) v = 10u + (unsigned)((c | 0x20) - 'a');
+    else v = 15;
+    if ((v >> (3 - i % 4)) & 1u) return 0;
+  }
+  return 1;
+}
+
+int pow_hash_blocks(pow_ctx* ctx, const pow_block* blocks, size_t n, uint8_t* digests, char* hex) {
+  if (!ctx || (!blocks && n)) return fail(POW_EINVAL, "null");
+  if (n == 0) return POW_OK;
+  if (n > (1u << 24)) return fail(POW_EINVAL, "batch too large");
+  if (int rc = set_dev(ctx)) return rc;
+  if (n > ctx->hash_cap) {
+    (void)hipFree(ctx->d_msgs);
+    (void)hipFree(ctx->d_dig);
+    ctx->d_msgs = nullptr;
+    ctx->d_dig = nullptr;
+    ctx->hash_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_msgs, n * 320));
+    HIP_OK(hipMalloc(&ctx->d_dig, n * 32));
+    ctx->hash_cap = n;
+  }
+  std::vector<uint32_t> words(n * 80);
+  for (size_t i = 0; i < n; ++i) {
+    uint8_t m[320];
+    padded_message(&blocks[i], m);
+    for (int k = 0; k < 80; ++k) words[i * 80 + k] = be32(m + 4 * k);
+  }
+  HIP_OK(hipMemcpyAsync(ctx->d_msgs, words.data(), n * 320, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIP_OK(pow_launch_hash((uint32_t)n, ctx->stream, ctx->d_msgs, ctx->d_dig));
+  HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
+  std::vector<uint32_t> dg(n * 8);
+  HIP_OK(hipMemcpyAsync(dg.data(), ctx->d_dig, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->stats = pow_stats{ms, 1u, (uint64_t)n};
+  static const char hexd[] = "0123456789abcdef";  // picosha2.h:141-150 (lowercase)
+  for (size_t i = 0; i < n; ++i) {
+    uint8_t d[32];
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t v = dg[i * 8 + k];
+      d[4 * k] = (uint8_t)(v >> 24);
+      d[4 * k + 1] = (uint8_t)(v >> 16);
+      d[4 * k + 2] = (uint8_t)(v >> 8);
+      d[4 * k + 3] = (uint8_t)v;
+    }
+    if (digests) memcpy(digests + 32 * i, d, 32);
+    if (hex) {
+      char* hx = hex + 65 * i;
+      for (int k = 0; k < 32; ++k) {
+        hx[2 * k] = hexd[d[k] >> 4];
+        hx[2 * k + 1] = hexd[d[k] & 15];
+      }
+      hx[64] = 0;
+    }
+  }
+  return POW_OK;
+}
+
+int pow_hash_block(pow_ctx* ctx, const pow_block* b, uint8_t digest[32], char hex[65]) {
+  return pow_hash_blocks(ctx, b, 1, digest, hex);
+}
+
+int pow_sweep_device(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                     unsigned diff_bits, uint32_t* dev_out, size_t cap, size_t* n_found,
+                     uint64_t* min_ctr) {
+  if (!ctx) return fail(POW_EINVAL, "null ctx");
+  if (int rc = check_range(tmpl, ctr_start, ctr_count, diff_bits)) return rc;
+  if (ctr_count > (1ull << 32)) return fail(POW_EINVAL, "sweep count > 2^32");
+  if (cap && !dev_out) return fail(POW_EINVAL, "cap without buffer");
+  if (int rc = set_dev(ctx)) return rc;
+  ctx->stats = pow_stats{};
+  if (n_found) *n_found = 0;
+  if (min_ctr) *min_ctr = ~0ull;
+  if (ctr_count == 0) return POW_OK;
+  if (int rc = upload_consts(ctx, tmpl)) return rc;
+  const uint32_t cap32 = (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu);
+  if (int rc = run_search(ctx, ctr_start, ctr_count, diff_bits, 0, dev_out, cap32)) return rc;
+  if (n_found) *n_found = ctx->h_res->count;
+  if (min_ctr && ctx->h_res->min_rel != ~0ull) *min_ctr = ctr_start + ctx->h_res->min_rel;
+  return POW_OK;
+}
+
+int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+              unsigned diff_bits, uint32_t* out_ctrs, size_t cap, size_t* n_found) {
+  if (!ctx || !n_found) return fail(POW_EINVAL, "null");
+  if (cap && !out_ctrs) return fail(POW_EINVAL, "cap without buffer");
+  if (int rc = set_dev(ctx)) return rc;
+  if (cap > ctx->out_cap) {
+    (void)hipFree(ctx->d_out);
+    ctx->d_out = nullptr;
+    ctx->out_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_out, cap * sizeof(uint32_t)));
+    ctx->out_cap = cap;
+  }
+  size_t n = 0;
+  uint64_t mn = 0;
+  int rc = pow_sweep_device(ctx, tmpl, ctr_start, ctr_count, diff_bits, cap ? ctx->d_out : nullptr,
+                            cap, &n, &mn);
+  if (rc) return rc;
+  *n_found = n;
+  const size_t got = std::min(n, cap);
+  if (got) {
+    HIP_OK(hipMemcpy(out_ctrs, ctx->d_out, got * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::sort(out_ctrs, out_ctrs + got);
+  }
+  return n > cap ? fail(POW_ENOSPC, "%zu solutions > cap %zu", n, cap) : POW_OK;
+}
+
+int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+             unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+             pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
+  if (!ctx || !out) return fail(POW_EINVAL, "null");
+  if (int rc = check_range(tmpl, ctr_start, ctr_count, diff_bits)) return rc;
+  if (int rc = set_dev(ctx)) return rc;
+  ctx->stats = pow_stats{};
+  if (hashes_done) *hashes_done = 0;
+  if (int rc = upload_consts(ctx, tmpl)) return rc;
+  // Sub-rounds grow geometrically from ~4x the expected trials per solution
+  // (short time-to-block at low difficulty) to 2^30 counters (~0.1 s), the
+  // granularity at which the cancel word is polled.
+  const unsigned dcap = diff_bits > 40 ? 40 : diff_bits;
+  uint64_t step = std::max<uint64_t>(62ull * 64, 1ull << std::min(dcap + 2, 30u));
+  uint64_t done = 0;
+  while (done < ctr_count) {
+    if (cancel_word && *cancel_word != epoch) break;
+    const uint64_t n = std::min(step, ctr_count - done);
+    const uint64_t s0 = ctr_start + done;
+    if (int rc = run_search(ctx, s0, n, diff_bits, 1, nullptr, 0)) return rc;
+    done += n;
+    if (ctx->h_res->min_rel != ~0ull) {
+      const uint64_t ctr = s0 + ctx->h_res->min_rel;
+      *out = *tmpl;
+      pow_nonce_from_counter(ctr, out->nonce);
+      char hx[65];
+      const pow_stats keep = ctx->stats;
+      if (int rc = pow_hash_blocks(ctx, out, 1, nullptr, hx)) return rc;
+      ctx->stats = keep;
+      memcpy(out->block_hash, hx, 65);  // strcpy semantics (node.cpp:318)
+      if (found_ctr) *found_ctr = ctr;
+      if (hashes_done) *hashes_done = ctx->stats.hashes;
+      return 1;
+    }
+    step = std::min<uint64_t>(step * 4, 1ull << 30);
+  }
+  if (hashes_done) *hashes_done = ctx->stats.hashes;
+  return 0;
+}
+
+int pow_dev_alloc(pow_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out) return fail(POW_EINVAL, "null");
+  *out = nullptr;
+  if (int rc = set_dev(ctx)) return rc;
+  HIP_OK(hipMalloc(out, bytes ? bytes : 1));
+  return POW_OK;
+}
+
+int pow_dev_free(pow_ctx* ctx, void* p) {
+  if (!ctx) return fail(POW_EINVAL, "null");
+  if (int rc = set_dev(ctx)) return rc;
+  HIP_OK(hipFree(p));
+  return POW_OK;
+}
+
+int pow_dev_read(pow_ctx* ctx, const void* dev, void* host, size_t bytes) {
+  if (!ctx || (bytes && (!dev || !host))) return fail(POW_EINVAL, "null");
+  if (int rc = set_dev(ctx)) return rc;
+  HIP_OK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return POW_OK;
+}
+
+}  // extern "C"

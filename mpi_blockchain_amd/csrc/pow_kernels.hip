@@ -1,0 +1,240 @@
+// gfx950 kernels of the proof-of-work hot path.
+//
+// K1  pow_search<MODE, FULL>  — the mining inner loop of proof_of_work
+//     (node.cpp:302-308): nonce (block.cpp:61-72) -> 270-byte message
+//     (block.cpp:79-88) -> SHA-256 (picosha2.h:88-136, 5 chunks) ->
+//     leading-zero-bit test (block.cpp:91-96, trap T3) for every counter of a
+//     range.  MODE 0 = sweep (record every solution), 1 = mine (lowest
+//     solving counter, early exit).  FULL = difficulty > 32 bits.
+// K2  pow_hash_kernel — block_to_hash (block.cpp:74-77) for a batch of blocks.
+//
+// Work decomposition of K1 (DESIGN.md "Kernel K1"): counter c = 62*P + j.
+//   * one LANE owns a prefix P (nonce chars 0..7, message words W1, W2);
+//     the prefix-dependent rounds 1-2 and schedule terms are computed once
+//     per prefix, then
+//   * the lane loops over j = 0..61 (the last nonce char, word W3) — j is
+//     wave-uniform, so W3 and every term derived from it are scalar loads.
+//   Per trial the lane runs chunk-0 rounds 3..63 and chunks 1-4 (whose K+W
+//   come from SGPRs: template-constant schedule) — no memory traffic.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pow_template.h"
+#include "sha256_dev.h"
+
+using namespace powdev;
+
+
+namespace {
+
+__device__ __forceinline__ uint32_t digit_char(uint32_t d) {
+  // block.cpp:61-72: 0-25 'a'+d, 26-51 'A'+d-26, 52-61 '0'+d-52
+  return d + (d < 26u ? 97u : (d < 52u ? 39u : 0xFFFFFFFCu));
+}
+
+__device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// Make a wave-uniform pointer opaque and data-dependent on `dep`, so the
+// scalar loads through it can neither be hoisted out of the j-loop (which
+// spills SGPRs: 256 K+W words do not fit) nor scheduled before `dep` exists.
+template <typename Tp>
+__device__ __forceinline__ const Tp* pin(const Tp* p, uint32_t dep) {
+  asm volatile("" : "+s"(p) : "v"(dep));
+  return p;
+}
+
+// Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
+__device__ __forceinline__ bool full_test(const uint32_t H[8], uint32_t d) {
+  uint32_t lz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (lz == 32u * i) lz += (H[i] == 0u) ? 32u : (uint32_t)__builtin_clz(H[i]);
+  }
+  return lz >= d;
+}
+
+}  // namespace
+
+template <int MODE, bool FULL>
+__global__ __launch_bounds__(256) void pow_search(const PowConsts* __restrict__ C, PowLaunch L,
+                                                  uint32_t* __restrict__ out,
+                                                  PowResult* __restrict__ res) {
+  const uint32_t T = gridDim.x * 256u;
+  const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+  uint32_t iters = 0;
+
+  for (uint32_t rbase = 0; rbase < L.n_prefix; rbase += T) {
+    if (MODE == 1) {
+      // Early exit: every counter of this and later iterations is >= 62*rbase - off0.
+      unsigned long long f =
+          __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      f = uniform64(f);
+      long long lo = (long long)rbase * 62 - (long long)L.off0;
+      if (lo > 0 && f < (unsigned long long)lo) break;
+    }
+    ++iters;
+    const uint32_t r = rbase + gid;
+
+    // ---- per-prefix: nonce digits 0..7 = base digits + r (base 62) ----
+    uint32_t dg[8];
+    {
+      uint32_t x = r, carry = 0;
+#pragma unroll
+      for (int i = 7; i >= 0; --i) {
+        uint32_t q = x / 62u;
+        uint32_t s = L.base_digit[i] + (x - q * 62u) + carry;
+        x = q;
+        carry = s >= 62u ? 1u : 0u;
+        dg[i] = carry ? s - 62u : s;
+      }
+    }
+    const uint32_t W1 = (digit_char(dg[0]) << 24) | (digit_char(dg[1]) << 16) |
+                        (digit_char(dg[2]) << 8) | digit_char(dg[3]);
+    const uint32_t W2 = (digit_char(dg[4]) << 24) | (digit_char(dg[5]) << 16) |
+                        (digit_char(dg[6]) << 8) | digit_char(dg[7]);
+
+    // ---- per-prefix: chunk-0 rounds 1, 2 and the prefix schedule terms ----
+    St s2{C->st0[0], C->st0[1], C->st0[2], C->st0[3], C->st0[4], C->st0[5], C->st0[6], C->st0[7]};
+    round_k_w(s2, K[1], W1);
+    round_k_w(s2, K[2], W2);
+    const uint32_t W16 = C->u16 + ssig0(W1);
+    const uint32_t W17 = C->u17 + ssig0(W2) + W1;
+    const uint32_t c18 = ssig1(W16) + W2;
+    const uint32_t c19 = ssig1(W17) + C->u19;
+    const uint32_t c23 = W16 + C->u23;
+    const uint32_t c24 = W17 + C->u24;
+    const uint32_t c31 = ssig0(W16) + C->w15;
+    const uint32_t c32 = ssig0(W17) + W16;
+
+    for (uint32_t j = 0; j < POW_J; ++j) {
+      // ---------------- chunk 0, rounds 3..63 ----------------
+      const PowConsts* C0 = pin(C, s2.a ^ j);
+      St s = s2;
+      round_kw(s, C0->kw3[j]);
+#pragma unroll
+      for (int i = 4; i < 16; ++i) round_kw(s, C0->kw0[i]);
+      uint32_t w[64];
+      w[16] = W16;
+      w[17] = W17;
+      round_k_w(s, K[16], W16);
+      round_k_w(s, K[17], W17);
+      w[18] = c18 + C0->u18[j];
+      round_k_w(s, K[18], w[18]);
+      w[19] = c19 + C0->w3[j];
+      round_k_w(s, K[19], w[19]);
+      w[20] = ssig1(w[18]) + C0->u20;
+      round_k_w(s, K[20], w[20]);
+      w[21] = ssig1(w[19]) + C0->u21;
+      round_k_w(s, K[21], w[21]);
+      w[22] = ssig1(w[20]) + C0->u22;
+      round_k_w(s, K[22], w[22]);
+      w[23] = ssig1(w[21]) + c23;
+      round_k_w(s, K[23], w[23]);
+      w[24] = ssig1(w[22]) + c24;
+      round_k_w(s, K[24], w[24]);
+#pragma unroll
+      for (int i = 25; i < 31; ++i) {
+        w[i] = ssig1(w[i - 2]) + w[i - 7] + C0->u25[i - 25];
+        round_k_w(s, K[i], w[i]);
+      }
+      w[31] = ssig1(w[29]) + w[24] + c31;
+      round_k_w(s, K[31], w[31]);
+      w[32] = ssig1(w[30]) + w[25] + c32;
+      round_k_w(s, K[32], w[32]);
+#pragma unroll
+      for (int i = 33; i < 64; ++i) {
+        w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+        round_k_w(s, K[i], w[i]);
+      }
+      uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
+                       IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};
+
+      // ---------------- chunks 1..3: constant schedule ----------------
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint32_t* kw = pin(C->kw[c], H[0]);
+        St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+#pragma unroll
+        for (int i = 0; i < 64; ++i) round_kw(t, kw[i]);
+        H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
+        H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
+      }
+      // ---------------- chunk 4 (last): only what the test needs ----------------
+      const uint32_t* kw4 = pin(C->kw[3], H[0]);
+      St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+#pragma unroll
+      for (int i = 0; i < 64; ++i) round_kw(t, kw4[i]);
+      const uint32_t h0 = H[0] + t.a;
+
+      bool hit = h0 <= L.thr;
+      if (FULL && hit) {
+        uint32_t D[8] = {h0, H[1] + t.b, H[2] + t.c, H[3] + t.d,
+                         H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
+        hit = full_test(D, L.diff);
+      }
+      if (__builtin_expect(hit, 0)) {
+        const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
+        if (rel < L.count) {  // also rejects j < off0 at r = 0 (wraps) and lanes past the end
+          atomicMin(&res->min_rel, rel);
+          if (MODE == 0) {
+            uint32_t idx = atomicAdd(&res->count, 1u);
+            if (idx < L.cap) out[idx] = (uint32_t)rel;
+          }
+        }
+      }
+    }
+  }
+  if (MODE == 1) {
+    // trials computed by this wave (lanes of a wave run the same iterations)
+    if ((threadIdx.x & 63u) == 0)
+      atomicAdd(&res->hashes, (unsigned long long)iters * 64ull * POW_J);
+  }
+}
+
+template __global__ void pow_search<0, false>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+template __global__ void pow_search<0, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+template __global__ void pow_search<1, false>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+template __global__ void pow_search<1, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+
+// K2: block_to_hash for n blocks; `msgs` holds each block's 270-byte message
+// already padded on the host to 320 bytes (80 big-endian words).
+__global__ __launch_bounds__(64) void pow_hash_kernel(const uint32_t* __restrict__ msgs, uint32_t n,
+                                                      uint32_t* __restrict__ digests) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = IV[k];
+  const uint32_t* m = msgs + (size_t)i * 80u;
+  for (int c = 0; c < 5; ++c) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = m[c * 16 + k];
+    compress(h, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) digests[(size_t)i * 8u + k] = h[k];
+}
+
+// ---- host-side launch wrappers (called from pow_api.cpp) ----
+extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream,
+                                          const PowConsts* C, const PowLaunch& L, uint32_t* out,
+                                          PowResult* res) {
+  dim3 g(grid), b(256);
+  if (mode == 0 && !full) hipLaunchKernelGGL((pow_search<0, false>), g, b, 0, stream, C, L, out, res);
+  else if (mode == 0) hipLaunchKernelGGL((pow_search<0, true>), g, b, 0, stream, C, L, out, res);
+  else if (!full) hipLaunchKernelGGL((pow_search<1, false>), g, b, 0, stream, C, L, out, res);
+  else hipLaunchKernelGGL((pow_search<1, true>), g, b, 0, stream, C, L, out, res);
+  return hipGetLastError();
+}
+
+extern "C++" hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs,
+                                        uint32_t* digests) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pow_hash_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, msgs, n, digests);
+  return hipGetLastError();
+}

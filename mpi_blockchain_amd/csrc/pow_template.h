@@ -1,0 +1,72 @@
+// Per-template constants of the gfx950 mining kernel (host precompute).
+//
+// The reference hashes, per trial, the 270-byte message of block_to_str
+// (block.cpp:79-88): [idx&ff, owner&ff, diff&ff, created_at&ff] nonce[0..9]
+// prev[0..255], padded by picosha2 (picosha2.h:201-218) to 320 bytes = five
+// 64-byte chunks.  With counter nonces (include/pow_gpu.h) the words are
+//
+//   chunk 0:  W0      = header bytes                         uniform
+//             W1, W2  = nonce[0..3], nonce[4..7]             per lane: the counter's
+//                                                            "prefix" c / 62
+//             W3      = [nonce[8], nonce[9]=0, prev0, prev1] per inner-loop step j = c % 62,
+//                                                            wave-uniform
+//             W4..W15 = prev[2..49]                          uniform
+//   chunks 1-4: prev[50..255] + 0x80 + zeros + bit length 2160   uniform
+//
+// so chunks 1-4 have a template-constant message schedule: their K[i]+W[i]
+// (4 x 64 words) are folded on the host and streamed to the kernel through
+// scalar loads; round 0 of chunk 0 is uniform and precomputed; the chunk-0
+// schedule terms that do not depend on the lane's W1/W2 or on j are folded
+// here too (u16.. below).  See DESIGN.md "Kernel K1".
+#pragma once
+#include <stdint.h>
+
+#define POW_J 62 /* inner-loop steps per prefix: the last base-62 nonce digit */
+
+struct PowConsts {
+  uint32_t kw[4][64];   // chunks 1..4: K[i] + W[i]                        (1024 B)
+  uint32_t st0[8];      // chunk-0 working variables after round 0
+  uint32_t kw0[16];     // chunk 0: K[i] + W[i] for i = 4..15 (0..3 unused)
+  uint32_t w0, w1_unused, w2_unused, w3lo;  // W0; low 24 bits of W3 (nonce[9], prev0, prev1)
+  // Uniform partial sums of the chunk-0 schedule (sigma terms of uniform words):
+  uint32_t u16;  // s1(W14) + W9 + W0            -> W16 = u16 + s0(W1)
+  uint32_t u17;  // s1(W15) + W10                -> W17 = u17 + s0(W2) + W1
+  uint32_t u19;  // W12 + s0(W4)                 -> W19 = s1(W17) + u19 + W3
+  uint32_t u20, u21, u22;        // W_{i-7} + s0(W_{i-15}) + W_{i-16}, i = 20..22
+  uint32_t u23, u24;             // s0(W_{i-15}) + W_{i-16}, i = 23, 24 (W16/W17 added per lane)
+  uint32_t u25[6];               // s0(W_{i-15}) + W_{i-16}, i = 25..30
+  uint32_t w15;                  // W15 (for W31 = s1(W29) + W24 + s0(W16) + W15)
+  uint32_t pad[3];
+  // Per inner step j (the nonce's last char), wave-uniform:
+  uint32_t kw3[POW_J];   // K[3] + W3(j)
+  uint32_t u18[POW_J];   // s0(W3(j)) + W11          -> W18 = s1(W16) + W2 + u18[j]
+  uint32_t w3[POW_J];    // W3(j)                      -> W19
+};
+
+// Launch parameters of one kernel dispatch.
+struct PowLaunch {
+  uint32_t base_digit[8];  // base-62 digits of the first prefix P0 (nonce[0..7])
+  uint32_t n_prefix;       // prefixes P0 .. P0 + n_prefix - 1
+  uint32_t off0;           // ctr_start - 62*P0   (0..61)
+  uint64_t count;          // counters requested (relative range [0, count))
+  uint32_t thr;            // d <= 32: solution iff H0 <= thr;  d > 32: thr = 0
+  uint32_t diff;           // difficulty in bits
+  uint32_t cap;            // sweep output capacity
+  uint32_t mode;           // 0 = sweep (record all), 1 = mine (lowest + early exit)
+};
+
+// Device-side result words of one launch (zeroed / ~0 before each launch).
+struct PowResult {
+  unsigned long long min_rel;  // lowest solving (counter - ctr_start); ~0 = none
+  unsigned long long hashes;   // mine mode: trials actually computed
+  unsigned int count;          // number of solutions (sweep)
+  unsigned int pad[3];
+};
+
+#ifdef __cplusplus
+extern "C++" {
+struct pow_block;
+// Fill PowConsts from a template block (nonce field ignored).
+void pow_build_consts(const struct pow_block* tmpl, PowConsts* out);
+}
+#endif

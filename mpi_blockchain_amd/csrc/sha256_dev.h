@@ -1,0 +1,85 @@
+// SHA-256 building blocks for gfx950 (CDNA4) device code.
+//
+// FIPS 180-4 SHA-256 as picosha2 implements it (picosha2.h:46-136): 64-round
+// compression over big-endian words.  Every primitive maps to ONE gfx950 VALU
+// instruction:
+//   rotr            v_alignbit_b32  (x:x >> n)
+//   3-way xor       v_bitop3_b32 0x96
+//   Ch(e,f,g)       v_bitop3_b32 0xCA   (e ? f : g)
+//   Maj(a,b,c)      v_bitop3_b32 0xE8
+//   a+b+c           v_add3_u32          (formed by the compiler)
+// so a round is 14 VALU ops and a schedule word 10 (DESIGN.md "op count").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace powdev {
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t bsig0(uint32_t a) { return xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
+__device__ __forceinline__ uint32_t bsig1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
+__device__ __forceinline__ uint32_t ssig0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
+__device__ __forceinline__ uint32_t ssig1(uint32_t x) { return xor3(rotr(x, 17), rotr(x, 19), x >> 10); }
+
+// picosha2.h:46-57
+__device__ constexpr uint32_t K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+// picosha2.h:59-61
+__device__ constexpr uint32_t IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                       0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+// Working variables of one compression.  Rounds "rename" instead of moving:
+// in the fully unrolled code the shifts below are SSA renames, not v_mov.
+struct St {
+  uint32_t a, b, c, d, e, f, g, h;
+};
+
+// One round whose K[i]+W[i] is a single (usually wave-uniform, SGPR) value.
+__device__ __forceinline__ void round_kw(St& s, uint32_t kw) {
+  uint32_t t1 = s.h + bsig1(s.e) + ch(s.e, s.f, s.g) + kw;
+  uint32_t t2 = bsig0(s.a) + maj(s.a, s.b, s.c);
+  s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+  s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+// One round with separate K (uniform) and W (per lane): add3(h,S1,Ch), add3(.,K,W).
+__device__ __forceinline__ void round_k_w(St& s, uint32_t k, uint32_t w) {
+  uint32_t t1 = s.h + bsig1(s.e) + ch(s.e, s.f, s.g) + k + w;
+  uint32_t t2 = bsig0(s.a) + maj(s.a, s.b, s.c);
+  s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+  s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
+// Generic compression of one chunk with an in-register schedule (used by the
+// single-hash kernel K2; not on the mining hot loop).
+__device__ __forceinline__ void compress(uint32_t h[8], const uint32_t win[16]) {
+  uint32_t w[64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = win[i];
+#pragma unroll
+  for (int i = 16; i < 64; ++i) w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+  St s{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+#pragma unroll
+  for (int i = 0; i < 64; ++i) round_k_w(s, K[i], w[i]);
+  h[0] += s.a; h[1] += s.b; h[2] += s.c; h[3] += s.d;
+  h[4] += s.e; h[5] += s.f; h[6] += s.g; h[7] += s.h;
+}
+
+}  // namespace powdev

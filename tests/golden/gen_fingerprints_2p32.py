@@ -1,0 +1,48 @@
+"""Generate the full-window fingerprints of tests/golden/fingerprints_2p32.json.
+
+Template S0 (index=1, owner=0, difficulty=9, created_at=1700000000, prev = 256
+zero bytes), counters [0, 2^32), difficulty ladder d = 9, 13, 17, 21, 25 bits.
+Fingerprint = sha256 of the ascending solving counters as little-endian u32.
+
+Computed with the C restatement (oracle/liboracle.so, itself pinned against the
+reference's own block_to_hash/solves_problem on the 2^20 windows of
+golden.json) in one pass at d=9, recording each solution's leading-zero-bit
+count; the higher rungs are the subsets with lz >= d.  Cross-checked against the
+independent hashlib computation recorded in SURVEY.md §8c (same counts and
+hashes).  Runtime: ~20 min on 8 cores.
+
+    python tests/golden/gen_fingerprints_2p32.py [threads]
+"""
+import ctypes, hashlib, json, os, sys, time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle.oracle import OBlock, Oracle, make_oblock  # noqa: E402
+
+threads = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+O = Oracle()
+L = O.L
+L.oracle_sweep_lz.argtypes = [ctypes.POINTER(OBlock), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                              ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint8),
+                              ctypes.c_size_t, ctypes.c_int]
+L.oracle_sweep_lz.restype = ctypes.c_size_t
+S0 = make_oblock(1, 0, 9, 1700000000, b"")
+cap = 9_000_000
+ctr = np.zeros(cap, np.uint32)
+lz = np.zeros(cap, np.uint8)
+t = time.time()
+n = L.oracle_sweep_lz(ctypes.byref(S0), 0, 1 << 32, 9, ctr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                      lz.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), cap, threads)
+assert n <= cap
+ctr, lz = ctr[:n], lz[:n]
+out = {"template": "S0", "start": 0, "count": 1 << 32, "seconds": round(time.time() - t, 1), "ladder": {}}
+for d in (9, 13, 17, 21, 25):
+    sel = ctr[lz >= d]
+    out["ladder"][str(d)] = {"count": int(sel.size),
+                             "sha256_le_u32": hashlib.sha256(sel.astype("<u4").tobytes()).hexdigest(),
+                             "first": [int(x) for x in sel[:8]]}
+json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "fingerprints_2p32.json"), "w"),
+          indent=1)
+print(json.dumps(out))

@@ -1,0 +1,194 @@
+"""GPU parity: the gfx950 path (through the C ABI) vs the reference's own
+outputs (tests/golden/golden.json, generated from /root/reference's block.cpp +
+picosha2.h) — bit-exact digests and identical solution SETS.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from mpi_blockchain_amd._lib import COUNTER_LIMIT, PowError
+from mpi_blockchain_amd.block import block_to_str, field, nonce_from_counter
+from mpi_blockchain_amd.miner import GpuMiner, block_hex, refresh_template
+
+from helpers import block_from_random, block_from_template, with_nonce
+
+pytestmark = pytest.mark.gpu
+
+
+def fp(arr) -> str:
+    return hashlib.sha256(np.asarray(arr, dtype="<u4").tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def miner():
+    m = GpuMiner(0)
+    yield m
+    m.close()
+
+
+@pytest.fixture(scope="module")
+def miner_full():
+    """A context whose every launch uses the d > 32 kernel variant."""
+    os.environ["POW_FORCE_FULL"] = "1"
+    try:
+        m = GpuMiner(0)
+    finally:
+        os.environ.pop("POW_FORCE_FULL", None)
+    yield m
+    m.close()
+
+
+def test_device_is_gfx950(miner):
+    info = miner.device_info()
+    assert info["cu_count"] > 0
+
+
+def test_edge_counter_digests(miner, golden, templates):
+    """block_to_hash on the GPU (K2) for every template x edge counter."""
+    blocks, want = [], []
+    for e in golden["digests"]:
+        b = block_from_template(templates[e["template"]])
+        n = nonce_from_counter(e["counter"])
+        assert n[:9].decode() == e["nonce"]
+        blocks.append(with_nonce(b, n))
+        want.append(e["hex"])
+    assert miner.hash_blocks(blocks) == want
+
+
+def test_random_block_digests(miner, golden):
+    blocks = [block_from_random(e) for e in golden["random_blocks"]]
+    assert miner.hash_blocks(blocks) == [e["hex"] for e in golden["random_blocks"]]
+    # single-block form, raw digest bytes
+    b = blocks[0]
+    assert miner.digest(b).hex() == golden["random_blocks"][0]["hex"]
+
+
+def test_messages(golden, templates):
+    for name, hx in golden["messages"].items():
+        b = with_nonce(block_from_template(templates[name]), nonce_from_counter(0))
+        assert block_to_str(b).hex() == hx
+
+
+@pytest.mark.parametrize("variant", ["fast", "full"])
+def test_sweep_windows(miner, miner_full, golden, templates, variant):
+    """Deterministic counter sweep: identical solution set for every golden window."""
+    m = miner if variant == "fast" else miner_full
+    for w in golden["windows"]:
+        b = block_from_template(templates[w["template"]])
+        for d, s in w["sets"].items():
+            got = m.sweep(b, w["start"], w["count"], int(d))
+            assert got.size == s["count"], (w["template"], w["start"], d)
+            assert fp(got) == s["sha256_le_u32"], (w["template"], w["start"], d)
+            if s["count"] <= 4096:
+                assert got.tolist() == s["counters"]
+
+
+def test_sweep_count_and_min(miner, golden, templates):
+    for w in golden["windows"]:
+        b = block_from_template(templates[w["template"]])
+        for d, s in w["sets"].items():
+            n, mn = miner.sweep_count(b, w["start"], w["count"], int(d))
+            assert n == s["count"]
+            first = s["counters"][0] + w["start"] if s["count"] else None
+            assert mn == first
+
+
+def test_mine_lowest_counter(miner, golden, templates):
+    """pow_mine returns the LOWEST solving counter and a block the reference
+    would accept (nonce + strcpy'd hex, node.cpp:318)."""
+    for w in golden["windows"]:
+        b = block_from_template(templates[w["template"]])
+        for d, s in w["sets"].items():
+            r = miner.mine(b, w["start"], w["count"], int(d))
+            if s["count"] == 0:
+                assert r is None
+                continue
+            assert r is not None
+            assert r.counter == w["start"] + s["counters"][0]
+            assert field(r.block, "nonce") == nonce_from_counter(r.counter)
+            hx = block_hex(r.block)
+            assert hx == miner.block_to_hash(r.block)
+            assert field(r.block, "block_hash")[64] == 0
+            assert field(r.block, "block_hash")[65:] == field(b, "block_hash")[65:]
+            assert r.hashes >= r.counter - w["start"]
+
+
+def test_mine_from_every_offset(miner, golden, templates):
+    """Start the search inside a prefix (off0 = 1..61) just before a known solution."""
+    w = golden["windows"][0]  # S0 [0, 2^20)
+    b = block_from_template(templates[w["template"]])
+    sol = w["sets"]["9"]["counters"]
+    for k in range(0, 40):
+        target = sol[k]
+        start = max(0, target - (k % 62))
+        r = miner.mine(b, start, 4096, 9)
+        assert r is not None and r.counter == target
+
+
+def test_mine_no_solution_and_bounds(miner, templates):
+    b = block_from_template(templates["S0"])
+    assert miner.mine(b, 0, 200, 9) is None  # first S0 solution is 238
+    r = miner.mine(b, 0, 239, 9)
+    assert r is not None and r.counter == 238
+    with pytest.raises(PowError):
+        miner.mine(b, COUNTER_LIMIT - 10, 11, 9)
+    with pytest.raises(PowError):
+        miner.sweep(b, 0, (1 << 32) + 1, 9)
+    with pytest.raises(PowError):
+        miner.mine(b, 0, 10, 257)
+
+
+def test_difficulty_zero_and_enospc(miner, templates):
+    b = block_from_template(templates["S1"])
+    got = miner.sweep(b, 1000, 5000, 0, cap=5000)
+    assert got.tolist() == list(range(5000))
+    with pytest.raises(PowError) as ei:
+        miner.sweep(b, 0, 5000, 0, cap=100)
+    assert ei.value.code == -2
+
+
+def test_cancel_epoch(miner, templates):
+    b = block_from_template(templates["S2"])
+    miner.cancel()  # epoch moves: a call with the stale epoch stops at once
+    r = miner.mine(b, 0, 1 << 40, 60, epoch=(miner.epoch - 1) & 0xFFFFFFFF)
+    assert r is None
+    assert miner.stats()["launches"] == 0
+
+
+def test_chained_blocks_validate(miner):
+    """Mine three chained blocks with the GPU and check the chain the way the
+    receive side does (valid_new_block, block.cpp:13-25: recomputed hash ==
+    stored hash; prev == previous block_hash)."""
+    from mpi_blockchain_amd.block import make_block, solves_problem
+
+    last = make_block(0, 0, 9, 1700000000)  # genesis: block_hash zeroed (node.cpp:369)
+    chain = [last]
+    for k in range(3):
+        t = refresh_template(chain[-1], rank=k, difficulty=9, now=1700000000 + k)
+        r = miner.mine(t, 0, 1 << 30, 9)
+        assert r is not None
+        hx = block_hex(r.block)
+        assert solves_problem(hx, 9)
+        assert miner.block_to_hash(r.block) == hx
+        assert field(r.block, "previous_block_hash") == field(chain[-1], "block_hash")
+        chain.append(r.block)
+    assert [c.index for c in chain] == [0, 1, 2, 3]
+
+
+@pytest.mark.slow
+def test_full_window_2p32(miner, fingerprints, templates):
+    """BASELINE config 2 at full size: S0, counters [0, 2^32), d = 9..25 —
+    count and sha256 of the sorted solution list equal the CPU fingerprints."""
+    b = block_from_template(templates["S0"])
+    got = miner.sweep(b, 0, 1 << 32, 9, cap=9_000_000)
+    lad = fingerprints["ladder"]
+    assert got.size == lad["9"]["count"]
+    assert fp(got) == lad["9"]["sha256_le_u32"]
+    for d in ("13", "17", "21", "25"):
+        n, mn = miner.sweep_count(b, 0, 1 << 32, int(d))
+        assert n == lad[d]["count"]
+        assert mn == lad[d]["first"][0]
