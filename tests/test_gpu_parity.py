@@ -124,7 +124,8 @@ def test_mine_from_every_offset(miner, golden, templates):
     sol = w["sets"]["9"]["counters"]
     for k in range(0, 40):
         target = sol[k]
-        start = max(0, target - (k % 62))
+        prev = sol[k - 1] + 1 if k else 0
+        start = max(prev, target - (k % 62))
         r = miner.mine(b, start, 4096, 9)
         assert r is not None and r.counter == target
 

@@ -1,0 +1,108 @@
+"""Sharded search logic (mpi_blockchain_amd/shard.py), CPU only: static
+partition, min-counter winner, and a real world_size-2 run over
+torch.distributed gloo (the same all-reduce(MIN) code path the GPU ranks use
+over RCCL).  The per-rank search is the CPU oracle here — this tests the
+sharding and the collective, not the kernel."""
+import os
+import socket
+
+import pytest
+
+from mpi_blockchain_amd.shard import NONE, partition, sharded_mine
+from oracle.oracle import Oracle, make_oblock
+
+
+def test_partition_covers_range():
+    for count in (0, 1, 7, 62, 1000, 2**32 + 3):
+        for world in (1, 2, 3, 4, 8):
+            parts = [partition(100, count, r, world) for r in range(world)]
+            assert parts[0][0] == 100
+            for (s0, n0), (s1, _) in zip(parts, parts[1:]):
+                assert s0 + n0 == s1
+            assert sum(n for _, n in parts) == count
+
+
+def _simulated_world(search, start, count, round_size, world):
+    """Run every rank's search per round and reduce by hand (what RCCL does)."""
+    done = 0
+    while done < count:
+        n = min(round_size, count - done)
+        best = NONE
+        for r in range(world):
+            s, k = partition(start + done, n, r, world)
+            v = search(s, k) if k else None
+            best = min(best, NONE if v is None else v)
+        if best != NONE:
+            return best
+        done += n
+    return None
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_sharded_equals_single(world):
+    O = Oracle()
+    b = make_oblock(1, 0, 9, 1700000000, b"")
+
+    def search(s, n):
+        return O.mine(b, s, n, 13)
+
+    single = O.mine(b, 0, 1 << 15, 13)
+    # the first solution at d = 13 is 6399
+    assert single == 6399
+    for rs in (1000, 4096, 1 << 15):
+        assert _simulated_world(search, 0, 1 << 15, rs, world) == single
+    # rank-local view through sharded_mine with a fake reduction
+    calls = []
+
+    def fake_min(v):
+        calls.append(v)
+        return v
+
+    got = sharded_mine(search, fake_min, 6000, 1000, 1000, 0, 1)
+    assert got == 6399 and calls == [6399]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpi_blockchain_amd.shard import torch_allreduce_min
+
+    O = Oracle()
+    b = make_oblock(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
+    red = torch_allreduce_min()
+    res = []
+    for start, count, rs, d in ((0, 1 << 12, 1 << 12, 9), (300, 5000, 2048, 9), (0, 40000, 8192, 13)):
+        res.append(sharded_mine(lambda s, n: O.mine(b, s, n, d), red, start, count, rs, rank, world))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    O = Oracle()
+    b = make_oblock(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
+    want = [O.mine(b, 0, 1 << 12, 9), O.mine(b, 300, 5000, 9), O.mine(b, 0, 40000, 13)]
+    assert want[0] == 263  # golden: first S1 solution
+    assert out[0] == out[1] == want

@@ -1,14 +1,16 @@
 #!/bin/bash
-# Run GPU steps in sequence; each under its own time limit.  A step that ends
-# with a fault/abort/timeout (exit >= 124 or signal) stops the chain; a plain
+# Run one GPU step under its own time limit, output to gpurun_out/<name>.log.
+# A step that ends with a fault/abort/timeout (exit >= 124, or any code other
+# than 0/1/5) makes this script exit 100 so an `&&` chain stops there; a plain
 # test failure (exit 1) does not.
 #   tools/gpu_step.sh <name> <seconds> <command...>
 name=$1; secs=$2; shift 2
-mkdir -p gpurun_out
+out="${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out"
+mkdir -p "$out"
 echo "== $name: $*" >&2
-timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
 rc=$?
 echo "== $name rc=$rc" >&2
-tail -5 "gpurun_out/$name.log" >&2
-if [ $rc -ge 124 ] || [ $rc -gt 1 -a $rc -ne 5 ]; then exit 100; fi
+tail -4 "$out/$name.log" >&2
+if [ $rc -ge 124 ] || { [ $rc -gt 1 ] && [ $rc -ne 5 ]; }; then exit 100; fi
 exit 0

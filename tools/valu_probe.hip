@@ -1,0 +1,129 @@
+// VALU issue-rate probe for gfx950: which int32 instructions issue at the
+// SIMD-32 rate (wave64 in 2 cycles) and which at half of it?  Pins the
+// roofline "peak" of DESIGN.md.
+//
+//   hipcc --offload-arch=gfx950 -O3 tools/valu_probe.hip -o tools/valu_probe && tools/valu_probe
+//
+// Each kernel runs 8 independent chains per lane of one instruction (inline
+// asm, so the instruction is exactly the one named), 128 instructions per loop
+// iteration, at 1/2/4/8 waves per SIMD.  In-kernel clock = d(s_memtime) /
+// d(s_memrealtime) x 100 MHz.  Prints one JSON line per (op, waves/SIMD).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define CHAIN8(S)                                                   \
+  S(x0) S(x1) S(x2) S(x3) S(x4) S(x5) S(x6) S(x7)
+
+template <int OP>
+__device__ __forceinline__ void op(uint32_t& x, uint32_t y, uint32_t z) {
+  if constexpr (OP == 0) asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 1) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 2) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(x) : "v"(y));
+  if constexpr (OP == 3) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 4) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 5) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 6) asm volatile("v_add_f32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 7) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 8) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 9) asm volatile("v_lshrrev_b32_e32 %0, 3, %0" : "+v"(x));
+  if constexpr (OP == 10) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 11) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(x));
+  if constexpr (OP == 12) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "s"(y), "v"(z));
+  if constexpr (OP == 13) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+}
+
+static const char* kNames[] = {"v_add_u32_e32", "v_add3_u32", "v_alignbit_b32", "v_bitop3_b32",
+                               "v_xor_b32_e32", "v_fma_f32", "v_add_f32_e32", "v_lshl_or_b32",
+                               "v_xad_u32", "v_lshrrev_b32_e32", "v_add_u32_e64",
+                               "v_alignbit_b32(x,x)", "v_add3_u32(sgpr)", "v_and_or_b32"};
+
+template <int OP>
+__global__ __launch_bounds__(256) void probe(uint32_t seed, int iters, uint32_t* out,
+                                             unsigned long long* clk) {
+  uint32_t x0 = seed + threadIdx.x, x1 = x0 * 3u, x2 = x0 * 5u, x3 = x0 * 7u, x4 = x0 * 11u,
+           x5 = x0 * 13u, x6 = x0 * 17u, x7 = x0 * 19u;
+  uint32_t y = seed ^ 0x5bd1e995u, z = blockIdx.x + 0x3f800000u;
+  y = __builtin_amdgcn_readfirstlane(y);
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+#define S(v) op<OP>(v, y, z);
+      CHAIN8(S)
+#undef S
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t acc = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
+  if (acc == 0x9e3779b9u) out[0] = acc;
+  if (threadIdx.x == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+template <int OP>
+void run(int cus, int per_cu, uint32_t* out, unsigned long long* d_clk, unsigned long long* h_clk) {
+  const int grid = cus * per_cu, iters = 2000;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  double clock_ghz = 0;
+  for (int rep = 0; rep < 3; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(probe<OP>, dim3(grid), dim3(256), 0, 0, 0x1234u + rep, iters, out, d_clk);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      (void)hipMemcpy(h_clk, d_clk, 16 * grid, hipMemcpyDeviceToHost);
+      double sc = 0, sr = 0;
+      for (int b = 0; b < grid; ++b) { sc += (double)h_clk[2 * b]; sr += (double)h_clk[2 * b + 1]; }
+      clock_ghz = sc / sr * 0.1;  // realtime counter is 100 MHz
+    }
+  }
+  const double lane_ops = (double)grid * 256.0 * iters * 128.0 ;
+  const double waves_per_simd = per_cu;  // 256-thread block = 4 waves = 1 per SIMD
+  // cycles per wave64 instruction per SIMD, from the in-kernel clock
+  const double instr_per_simd = waves_per_simd * iters * 128.0;
+  const double cyc = (best * 1e-3) * clock_ghz * 1e9 / instr_per_simd;
+  printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"tlane_ops\": %.2f, "
+         "\"clock_ghz\": %.3f, \"cycles_per_wave_instr\": %.3f}\n",
+         kNames[OP], per_cu, best, lane_ops / (best * 1e-3) / 1e12, clock_ghz, cyc);
+  fflush(stdout);
+}
+
+int main() {
+  hipDeviceProp_t p;
+  (void)hipGetDeviceProperties(&p, 0);
+  const int cus = p.multiProcessorCount;
+  uint32_t* out;
+  unsigned long long *d_clk, *h_clk;
+  (void)hipMalloc(&out, 4);
+  (void)hipMalloc(&d_clk, 16 * cus * 8);
+  h_clk = (unsigned long long*)malloc(16 * cus * 8);
+  printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d}\n", p.gcnArchName, cus, p.clockRate);
+  for (int w : {8, 2, 1}) {
+    run<0>(cus, w, out, d_clk, h_clk);
+    run<1>(cus, w, out, d_clk, h_clk);
+    run<2>(cus, w, out, d_clk, h_clk);
+    run<3>(cus, w, out, d_clk, h_clk);
+    run<4>(cus, w, out, d_clk, h_clk);
+    run<5>(cus, w, out, d_clk, h_clk);
+    run<6>(cus, w, out, d_clk, h_clk);
+    run<7>(cus, w, out, d_clk, h_clk);
+    run<8>(cus, w, out, d_clk, h_clk);
+    run<9>(cus, w, out, d_clk, h_clk);
+    run<10>(cus, w, out, d_clk, h_clk);
+    run<11>(cus, w, out, d_clk, h_clk);
+    run<12>(cus, w, out, d_clk, h_clk);
+    run<13>(cus, w, out, d_clk, h_clk);
+  }
+  return 0;
+}
