@@ -23,6 +23,15 @@ static_assert(offsetof(pow_block, nonce) == 24, "layout");
 static_assert(offsetof(pow_block, previous_block_hash) == 34, "layout");
 static_assert(offsetof(pow_block, block_hash) == 290, "layout");
 static_assert(sizeof(PowConsts) % 4 == 0 && sizeof(PowConsts) < 4096, "consts");
+static_assert(offsetof(PowConsts, kw0) == 4 * PC_KW0, "PC_KW0");
+static_assert(offsetof(PowConsts, u20) == 4 * PC_U20, "PC_U20");
+static_assert(offsetof(PowConsts, u21) == 4 * (PC_U20 + 1), "PC_U21");
+static_assert(offsetof(PowConsts, u22) == 4 * (PC_U20 + 2), "PC_U22");
+static_assert(offsetof(PowConsts, u25) == 4 * PC_U25, "PC_U25");
+static_assert(offsetof(PowConsts, kw3) == 4 * PC_KW3, "PC_KW3");
+static_assert(offsetof(PowConsts, u18) == 4 * PC_U18, "PC_U18");
+static_assert(offsetof(PowConsts, w3) == 4 * PC_W3, "PC_W3");
+static_assert(offsetof(PowConsts, k) == 4 * PC_K, "PC_K");
 
 hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
                              const PowLaunch& L, uint32_t* out, PowResult* res);
@@ -130,6 +139,7 @@ void pow_build_consts(const pow_block* tmpl, PowConsts* C) {
   C->u24 = ssig0(W[9]) + W[8];
   for (int k = 0; k < 6; ++k) C->u25[k] = ssig0(W[10 + k]) + W[9 + k];
   C->w15 = W[15];
+  memcpy(C->k, kK, sizeof kK);
   for (unsigned j = 0; j < POW_J; ++j) {
     const uint32_t w3 = ((uint32_t)(uint8_t)digit_char(j) << 24) | C->w3lo;
     C->w3[j] = w3;
@@ -188,6 +198,7 @@ int make_launch(uint64_t start, uint64_t count, unsigned diff, uint32_t cap, uin
 }
 
 unsigned grid_for(const pow_ctx* ctx, uint32_t n_prefix) {
+  // one lane per prefix per chunk; no more workgroups than there are chunks
   const uint64_t want = ((uint64_t)n_prefix + 255) / 256;
   return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, ctx->grid_full));
 }

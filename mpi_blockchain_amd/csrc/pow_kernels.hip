@@ -38,13 +38,38 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// Make a wave-uniform pointer opaque and data-dependent on `dep`, so the
-// scalar loads through it can neither be hoisted out of the j-loop (which
-// spills SGPRs: 256 K+W words do not fit) nor scheduled before `dep` exists.
-template <typename Tp>
-__device__ __forceinline__ const Tp* pin(const Tp* p, uint32_t dep) {
+// Constant-address-space (addrspace 4) pointer: loads through it are known
+// read-only, so wave-uniform ones become scalar loads (s_load_dwordx*) into
+// SGPRs, which a VOP3 instruction reads as its one scalar operand.
+typedef const __attribute__((address_space(4))) uint32_t* cptr;
+
+__device__ __forceinline__ cptr as_const(const uint32_t* p) {
+  return (cptr)(const __attribute__((address_space(1))) uint32_t*)p;
+}
+
+// Make a uniform constant pointer opaque and data-dependent on `dep`, so the
+// scalar loads through it can neither be hoisted out of the j-loop (256 K+W
+// words do not fit in SGPRs: hoisting spills them) nor issued before `dep`.
+__device__ __forceinline__ cptr pin(cptr p, uint32_t dep) {
   asm volatile("" : "+s"(p) : "v"(dep));
   return p;
+}
+
+// 64 rounds of a chunk whose K+W are template constants, streamed through
+// SGPRs in groups of 16: group g+1's scalar loads are pinned behind the state
+// of round 16g+8, so at most two groups (32 SGPRs) are live and each group's
+// loads have 8 rounds to land.  (All 64 at once needs > 80 SGPRs, which cuts
+// residency from 8 to 6 workgroups per CU.)
+__device__ __forceinline__ void const_chunk(St& t, cptr kwbase, uint32_t dep) {
+#pragma unroll
+  for (int g = 0; g < 64; g += 16) {
+    cptr kw = pin(kwbase + g, dep);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      round_kw(t, kw[i]);
+      if (i == 7) dep = t.e;
+    }
+  }
 }
 
 // Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
@@ -59,17 +84,29 @@ __device__ __forceinline__ bool full_test(const uint32_t H[8], uint32_t d) {
 
 }  // namespace
 
+// Work distribution: each wave dequeues chunks of 64 consecutive prefixes (one
+// per lane) from res->next with one atomic, in increasing order.  Any grid
+// size and residency gives a tail of at most one chunk per wave (~2 ms), and
+// mine mode stays exact: a wave stops only when the lowest solution already
+// found is below its next chunk, and every lower chunk is owned by a wave
+// that is still running it.
+// 80 SGPRs: the measured admission rule for 256-thread workgroups on gfx950
+// (MI355X_MICROARCH.md "Residency") gives 8 per CU only at <= 80; at the
+// compiler's natural ~92 it is 7.
 template <int MODE, bool FULL>
-__global__ __launch_bounds__(256) void pow_search(const PowConsts* __restrict__ C, PowLaunch L,
-                                                  uint32_t* __restrict__ out,
-                                                  PowResult* __restrict__ res) {
-  const uint32_t T = gridDim.x * 256u;
-  const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search(
+    const PowConsts* __restrict__ C, PowLaunch L, uint32_t* __restrict__ out,
+    PowResult* __restrict__ res) {
+  const uint32_t lane = threadIdx.x & 63u;
   uint32_t iters = 0;
 
-  for (uint32_t rbase = 0; rbase < L.n_prefix; rbase += T) {
+  for (;;) {
+    uint32_t got = 0;
+    if (lane == 0) got = atomicAdd(&res->next, 64u);
+    const uint32_t rbase = __builtin_amdgcn_readfirstlane(got);
+    if (rbase >= L.n_prefix) break;
     if (MODE == 1) {
-      // Early exit: every counter of this and later iterations is >= 62*rbase - off0.
+      // Early exit: every counter of this and later chunks is >= 62*rbase - off0.
       unsigned long long f =
           __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       f = uniform64(f);
@@ -77,7 +114,7 @@ __global__ __launch_bounds__(256) void pow_search(const PowConsts* __restrict__ 
       if (lo > 0 && f < (unsigned long long)lo) break;
     }
     ++iters;
-    const uint32_t r = rbase + gid;
+    const uint32_t r = rbase + lane;
 
     // ---- per-prefix: nonce digits 0..7 = base digits + r (base 62) ----
     uint32_t dg[8];
@@ -112,43 +149,52 @@ __global__ __launch_bounds__(256) void pow_search(const PowConsts* __restrict__ 
 
     for (uint32_t j = 0; j < POW_J; ++j) {
       // ---------------- chunk 0, rounds 3..63 ----------------
-      const PowConsts* C0 = pin(C, s2.a ^ j);
+      cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
+      cptr J = pin(Cb, s2.a ^ j);  // per-j words and the chunk-0 uniform terms
       St s = s2;
-      round_kw(s, C0->kw3[j]);
+      round_kw(s, J[PC_KW3 + j]);
 #pragma unroll
-      for (int i = 4; i < 16; ++i) round_kw(s, C0->kw0[i]);
+      for (int i = 4; i < 16; ++i) round_kw(s, J[PC_KW0 + i]);
+      cptr Kp = pin(Cb + PC_K, s.e);  // K[16..63], streamed like the K+W words
       uint32_t w[64];
       w[16] = W16;
       w[17] = W17;
-      round_k_w(s, K[16], W16);
-      round_k_w(s, K[17], W17);
-      w[18] = c18 + C0->u18[j];
-      round_k_w(s, K[18], w[18]);
-      w[19] = c19 + C0->w3[j];
-      round_k_w(s, K[19], w[19]);
-      w[20] = ssig1(w[18]) + C0->u20;
-      round_k_w(s, K[20], w[20]);
-      w[21] = ssig1(w[19]) + C0->u21;
-      round_k_w(s, K[21], w[21]);
-      w[22] = ssig1(w[20]) + C0->u22;
-      round_k_w(s, K[22], w[22]);
+      round_k_w(s, Kp[16], W16);
+      round_k_w(s, Kp[17], W17);
+      w[18] = c18 + J[PC_U18 + j];
+      round_k_w(s, Kp[18], w[18]);
+      w[19] = c19 + J[PC_W3 + j];
+      round_k_w(s, Kp[19], w[19]);
+      w[20] = ssig1(w[18]) + J[PC_U20];
+      round_k_w(s, Kp[20], w[20]);
+      w[21] = ssig1(w[19]) + J[PC_U20 + 1];
+      round_k_w(s, Kp[21], w[21]);
+      w[22] = ssig1(w[20]) + J[PC_U20 + 2];
+      round_k_w(s, Kp[22], w[22]);
       w[23] = ssig1(w[21]) + c23;
-      round_k_w(s, K[23], w[23]);
+      round_k_w(s, Kp[23], w[23]);
       w[24] = ssig1(w[22]) + c24;
-      round_k_w(s, K[24], w[24]);
+      round_k_w(s, Kp[24], w[24]);
 #pragma unroll
       for (int i = 25; i < 31; ++i) {
-        w[i] = ssig1(w[i - 2]) + w[i - 7] + C0->u25[i - 25];
-        round_k_w(s, K[i], w[i]);
+        w[i] = ssig1(w[i - 2]) + w[i - 7] + J[PC_U25 + i - 25];
+        round_k_w(s, Kp[i], w[i]);
       }
       w[31] = ssig1(w[29]) + w[24] + c31;
-      round_k_w(s, K[31], w[31]);
+      round_k_w(s, Kp[31], w[31]);
+      cptr K2 = pin(Cb + PC_K, s.e);
       w[32] = ssig1(w[30]) + w[25] + c32;
-      round_k_w(s, K[32], w[32]);
+      round_k_w(s, K2[32], w[32]);
 #pragma unroll
-      for (int i = 33; i < 64; ++i) {
+      for (int i = 33; i < 48; ++i) {
         w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
-        round_k_w(s, K[i], w[i]);
+        round_k_w(s, K2[i], w[i]);
+      }
+      cptr K3 = pin(Cb + PC_K, s.e);
+#pragma unroll
+      for (int i = 48; i < 64; ++i) {
+        w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+        round_k_w(s, K3[i], w[i]);
       }
       uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
                        IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};
@@ -156,18 +202,14 @@ __global__ __launch_bounds__(256) void pow_search(const PowConsts* __restrict__ 
       // ---------------- chunks 1..3: constant schedule ----------------
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const uint32_t* kw = pin(C->kw[c], H[0]);
         St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-#pragma unroll
-        for (int i = 0; i < 64; ++i) round_kw(t, kw[i]);
+        const_chunk(t, as_const(C->kw[c]), H[0]);
         H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
         H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
       }
       // ---------------- chunk 4 (last): only what the test needs ----------------
-      const uint32_t* kw4 = pin(C->kw[3], H[0]);
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-#pragma unroll
-      for (int i = 0; i < 64; ++i) round_kw(t, kw4[i]);
+      const_chunk(t, as_const(C->kw[3]), H[0]);
       const uint32_t h0 = H[0] + t.a;
 
       bool hit = h0 <= L.thr;

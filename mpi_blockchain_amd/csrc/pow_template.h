@@ -41,7 +41,17 @@ struct PowConsts {
   uint32_t kw3[POW_J];   // K[3] + W3(j)
   uint32_t u18[POW_J];   // s0(W3(j)) + W11          -> W18 = s1(W16) + W2 + u18[j]
   uint32_t w3[POW_J];    // W3(j)                      -> W19
+  uint32_t k[64];        // K[0..63] (streamed from memory: VOP3 takes no literal)
 };
+
+// Word offsets into PowConsts for the kernel's constant-address-space loads.
+#define PC_KW0 (256 + 8)
+#define PC_U20 (PC_KW0 + 16 + 4 + 3)
+#define PC_U25 (PC_U20 + 5)
+#define PC_KW3 (PC_U25 + 6 + 4)
+#define PC_U18 (PC_KW3 + POW_J)
+#define PC_W3 (PC_U18 + POW_J)
+#define PC_K (PC_W3 + POW_J)
 
 // Launch parameters of one kernel dispatch.
 struct PowLaunch {
@@ -60,7 +70,8 @@ struct PowResult {
   unsigned long long min_rel;  // lowest solving (counter - ctr_start); ~0 = none
   unsigned long long hashes;   // mine mode: trials actually computed
   unsigned int count;          // number of solutions (sweep)
-  unsigned int pad[3];
+  unsigned int next;           // next prefix chunk to hand out (dynamic work queue)
+  unsigned int pad[2];
 };
 
 #ifdef __cplusplus

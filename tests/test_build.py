@@ -38,6 +38,14 @@ def kernel_body(isa: str, mangled_prefix: str) -> str:
     return m.group(2)
 
 
+def j_loop_body(isa: str, mangled_prefix: str) -> str:
+    """The per-trial j-loop: from its loop header to the next basic-block label."""
+    body = kernel_body(isa, mangled_prefix)
+    m = re.search(r"This Loop Header: Depth=2\n(.*?)\n\.LBB", body, flags=re.S)
+    assert m, "j-loop not found"
+    return m.group(1)
+
+
 def metadata(isa: str, name_prefix: str) -> dict:
     out = {}
     for blk in isa.split("  - .agpr_count")[1:]:
@@ -56,19 +64,23 @@ def metadata(isa: str, name_prefix: str) -> dict:
                                      "_Z10pow_searchILi0ELb1E", "_Z10pow_searchILi1ELb1E"])
 def test_no_spills_and_occupancy(isa, variant):
     md = metadata(isa, variant)
-    assert md["sgpr_spill_count"] == 0
+    # SGPRs are capped at 80 (8 workgroups/CU); the few spills this causes sit
+    # at chunk-dequeue level and in the rare hit path, never in the j-loop
+    # (test_j_loop_clean).
+    assert md["sgpr_spill_count"] <= 16
     assert md["vgpr_spill_count"] == 0
     assert md["private_segment_fixed_size"] == 0
     assert md["vgpr_count"] <= 64, md  # 8 waves / SIMD
 
 
-def test_inner_loop_valu_count(isa):
-    body = kernel_body(isa, "_Z10pow_searchILi0ELb0E")
-    ops = re.findall(r"^\s+(v_[a-z0-9_]+)", body, flags=re.M)
-    n = len(ops)
-    # prefix setup + j-loop body (one trial) + epilogue; the trial dominates
-    assert 4800 <= n <= 5200, n
-    # SGPR spills would show up as hundreds of v_writelane/v_readlane pairs
-    assert ops.count("v_readlane_b32") <= 8 and ops.count("v_writelane_b32") == 0
-    for needed in ("v_alignbit_b32", "v_bitop3_b32", "v_add3_u32"):
-        assert ops.count(needed) > 500, needed
+@pytest.mark.parametrize("variant", ["_Z10pow_searchILi0ELb0E", "_Z10pow_searchILi1ELb0E"])
+def test_j_loop_clean(isa, variant):
+    body = j_loop_body(isa, variant)
+    ops = re.findall(r"^\s+([sv]_[a-z0-9_]+|flat_\w+|global_\w+|scratch_\w+|buffer_\w+)", body, flags=re.M)
+    valu = [o for o in ops if o.startswith("v_")]
+    # one trial: chunk-0 rounds 3..63 + schedule, chunks 1-4, test ~= 4,850 VALU
+    assert 4700 <= len(valu) <= 5000, len(valu)
+    assert "v_readlane_b32" not in ops and "v_writelane_b32" not in ops
+    assert not [o for o in ops if o.startswith(("flat_", "global_", "scratch_", "buffer_"))], \
+        "the j-loop must take its constants through scalar loads only"
+    assert ops.count("s_load_dwordx16") >= 16
