@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CHAIN8(S)                                                   \
   S(x0) S(x1) S(x2) S(x3) S(x4) S(x5) S(x6) S(x7)
@@ -31,12 +32,195 @@ __device__ __forceinline__ void op(uint32_t& x, uint32_t y, uint32_t z) {
   if constexpr (OP == 11) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(x));
   if constexpr (OP == 12) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "s"(y), "v"(z));
   if constexpr (OP == 13) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 14) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 15) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 16) asm volatile("v_alignbyte_b32 %0, %0, %1, 1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 17) asm volatile("v_bfe_u32 %0, %0, 3, 17" : "+v"(x));
+  if constexpr (OP == 18) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 19) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 20) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(y));
+  if constexpr (OP == 21) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 22) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+}
+
+// Mixed streams: one "step" over the 8 chains; instruction order interleaves chains
+// so consecutive instructions are independent.
+#define AB(v) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(v) : "v"(y));
+#define B3(v) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v) : "v"(y), "v"(z));
+#define A3(v) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(v) : "v"(y), "v"(z));
+#define AD(v) asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(v) : "v"(y));
+#define SR(v) asm volatile("v_lshrrev_b32_e32 %0, 7, %0" : "+v"(v));
+#define SL(v) asm volatile("v_lshlrev_b32_e32 %0, 9, %0" : "+v"(v));
+#define XR(v) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(v) : "v"(y));
+#define ALL8(M) M(x0) M(x1) M(x2) M(x3) M(x4) M(x5) M(x6) M(x7)
+template <int P>
+__device__ __forceinline__ void pattern(uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t& x3, uint32_t& x4,
+                                        uint32_t& x5, uint32_t& x6, uint32_t& x7, uint32_t y, uint32_t z) {
+  if constexpr (P == 0) {  // SHA round mix: 6 alignbit, 4 bitop3, 2 add3, 2 add (x8 chains = 112)
+    ALL8(AB) ALL8(B3) ALL8(AB) ALL8(A3) ALL8(AB) ALL8(B3) ALL8(AD)
+    ALL8(AB) ALL8(B3) ALL8(AB) ALL8(A3) ALL8(AB) ALL8(B3) ALL8(AD)
+  }
+  if constexpr (P == 1) {  // alignbit : bitop3 = 1 : 1 (x8 = 128)
+    ALL8(AB) ALL8(B3) ALL8(AB) ALL8(B3) ALL8(AB) ALL8(B3) ALL8(AB) ALL8(B3)
+    ALL8(AB) ALL8(B3) ALL8(AB) ALL8(B3) ALL8(AB) ALL8(B3) ALL8(AB) ALL8(B3)
+  }
+  if constexpr (P == 2) {  // alignbit : add_u32 = 1 : 1
+    ALL8(AB) ALL8(AD) ALL8(AB) ALL8(AD) ALL8(AB) ALL8(AD) ALL8(AB) ALL8(AD)
+    ALL8(AB) ALL8(AD) ALL8(AB) ALL8(AD) ALL8(AB) ALL8(AD) ALL8(AB) ALL8(AD)
+  }
+  if constexpr (P == 4) {  // F1: round with adds split: 6 alignbit, 4 bitop3, 6 add (x8 = 128)
+    ALL8(AB) ALL8(B3) ALL8(AB) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AD)
+    ALL8(AB) ALL8(B3) ALL8(AB) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AD)
+  }
+  if constexpr (P == 5) {  // F2: all full rate: 12 shifts, 6 bitop3, 2 bitop3(ch/maj), 6 add (26 x8 = 208)
+    ALL8(SR) ALL8(SL) ALL8(SR) ALL8(B3) ALL8(SL) ALL8(SR) ALL8(SL) ALL8(B3) ALL8(XR) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(AD)
+    ALL8(SR) ALL8(SL) ALL8(SR) ALL8(B3) ALL8(SL) ALL8(SR) ALL8(SL) ALL8(B3) ALL8(XR) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(AD)
+  }
+  if constexpr (P == 6) {  // alignbit : bitop3 : add = 1 : 1 : 1 (x8 = 192)
+    ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD)
+    ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(AB) ALL8(B3) ALL8(AD)
+  }
+  if constexpr (P == 7) {  // alignbit runs of 24 then 24 full (same 1:1 ratio, coarse grouping)
+    ALL8(AB) ALL8(AB) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AD) ALL8(B3) ALL8(AD)
+    ALL8(AB) ALL8(AB) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AD) ALL8(B3) ALL8(AD)
+  }
+  if constexpr (P == 8) {  // alignbit : full = 1 : 3
+    ALL8(AB) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(B3)
+    ALL8(AB) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AB) ALL8(B3) ALL8(AD) ALL8(B3)
+  }
+  if constexpr (P == 9) {  // add3 : full = 1 : 1
+    ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD) ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD)
+    ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD) ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD)
+  }
+  if constexpr (P == 3) {  // bitop3 : add_u32 = 1 : 1 (all full rate)
+    ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD)
+    ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD)
+  }
+}
+static const int kPatLen[] = {112, 128, 128, 128, 128, 208, 192, 192, 128, 128};
+static const char* kPatNames[] = {"F0 round as built (6ab:4b3:2a3:2add)", "alignbit:bitop3 1:1",
+                                  "alignbit:add 1:1", "bitop3:add 1:1",
+                                  "F1 round, adds split (6ab:4b3:6add)", "F2 round, full-rate only (26 ops)",
+                                  "alignbit:bitop3:add 1:1:1", "alignbit runs of 24 / full 24",
+                                  "alignbit:full 1:3", "add3:full 1:1"};
+
+template <int P>
+__global__ __launch_bounds__(256) void probe_mix(uint32_t seed, int iters, uint32_t* out,
+                                                 unsigned long long* clk) {
+  uint32_t x0 = seed + threadIdx.x, x1 = x0 * 3u, x2 = x0 * 5u, x3 = x0 * 7u, x4 = x0 * 11u,
+           x5 = x0 * 13u, x6 = x0 * 17u, x7 = x0 * 19u;
+  uint32_t y = seed ^ 0x5bd1e995u, z = blockIdx.x + 0x3f800000u;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) pattern<P>(x0, x1, x2, x3, x4, x5, x6, x7, y, z);
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t acc = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
+  if (acc == 0x9e3779b9u) out[0] = acc;
+  if (threadIdx.x == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+template <int P>
+void run_mix(int cus, int per_cu, uint32_t* out, unsigned long long* d_clk, unsigned long long* h_clk) {
+  const int grid = cus * per_cu, iters = 2000;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  double clock_ghz = 0;
+  for (int rep = 0; rep < 3; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(probe_mix<P>, dim3(grid), dim3(256), 0, 0, 0x1234u + rep, iters, out, d_clk);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      (void)hipMemcpy(h_clk, d_clk, 16 * grid, hipMemcpyDeviceToHost);
+      double sc = 0, sr = 0;
+      for (int b = 0; b < grid; ++b) { sc += (double)h_clk[2 * b]; sr += (double)h_clk[2 * b + 1]; }
+      clock_ghz = sc / sr * 0.1;
+    }
+  }
+  const double instr_per_simd = (double)per_cu * iters * kPatLen[P];
+  const double cyc = (best * 1e-3) * clock_ghz * 1e9 / instr_per_simd;
+  printf("{\"pattern\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"clock_ghz\": %.3f, "
+         "\"cycles_per_wave_instr\": %.3f}\n", kPatNames[P], per_cu, best, clock_ghz, cyc);
+  fflush(stdout);
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void probe64(uint32_t seed, int iters, uint32_t* out,
+                                               unsigned long long* clk) {
+  unsigned long long x0 = seed + threadIdx.x, x1 = x0 * 3u, x2 = x0 * 5u, x3 = x0 * 7u;
+  unsigned long long x4 = x0 * 11u, x5 = x0 * 13u, x6 = x0 * 17u, x7 = x0 * 19u;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+#define S64(v)                                                                       \
+  if constexpr (OP == 0) asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(v));         \
+  if constexpr (OP == 1) asm volatile("v_lshlrev_b64 %0, 9, %0" : "+v"(v));         \
+  if constexpr (OP == 2) asm volatile("v_mov_b64_e32 %0, %0" : "+v"(v));             \
+  if constexpr (OP == 3) asm volatile("v_pk_mov_b32 %0, %0, %0 op_sel:[0,0]" : "+v"(v)); \
+  if constexpr (OP == 4) asm volatile("v_lshl_add_u64 %0, %0, 2, %0" : "+v"(v));
+      S64(x0) S64(x1) S64(x2) S64(x3) S64(x4) S64(x5) S64(x6) S64(x7)
+#undef S64
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long acc = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
+  if (acc == 0x9e3779b9u) out[0] = (uint32_t)acc;
+  if (threadIdx.x == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+static const char* k64Names[] = {"v_lshrrev_b64", "v_lshlrev_b64", "v_mov_b64", "v_pk_mov_b32",
+                                  "v_lshl_add_u64"};
+
+template <int OP>
+void run64(int cus, int per_cu, uint32_t* out, unsigned long long* d_clk, unsigned long long* h_clk) {
+  const int grid = cus * per_cu, iters = 2000;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  double clock_ghz = 0;
+  for (int rep = 0; rep < 3; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(probe64<OP>, dim3(grid), dim3(256), 0, 0, 0x1234u + rep, iters, out, d_clk);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      (void)hipMemcpy(h_clk, d_clk, 16 * grid, hipMemcpyDeviceToHost);
+      double sc = 0, sr = 0;
+      for (int b = 0; b < grid; ++b) { sc += (double)h_clk[2 * b]; sr += (double)h_clk[2 * b + 1]; }
+      clock_ghz = sc / sr * 0.1;
+    }
+  }
+  const double instr_per_simd = (double)per_cu * iters * 128.0;
+  const double cyc = (best * 1e-3) * clock_ghz * 1e9 / instr_per_simd;
+  printf("{\"op64\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"clock_ghz\": %.3f, "
+         "\"cycles_per_wave_instr\": %.3f}\n", k64Names[OP], per_cu, best, clock_ghz, cyc);
+  fflush(stdout);
 }
 
 static const char* kNames[] = {"v_add_u32_e32", "v_add3_u32", "v_alignbit_b32", "v_bitop3_b32",
                                "v_xor_b32_e32", "v_fma_f32", "v_add_f32_e32", "v_lshl_or_b32",
                                "v_xad_u32", "v_lshrrev_b32_e32", "v_add_u32_e64",
-                               "v_alignbit_b32(x,x)", "v_add3_u32(sgpr)", "v_and_or_b32"};
+                               "v_alignbit_b32(x,x)", "v_add3_u32(sgpr)", "v_and_or_b32", "v_bfi_b32",
+                               "v_perm_b32", "v_alignbyte_b32", "v_bfe_u32", "v_lshl_add_u32", "v_or3_b32",
+                               "v_cndmask_b32_e32", "v_sub_u32_e32", "v_mad_u32_u24"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void probe(uint32_t seed, int iters, uint32_t* out,
@@ -109,6 +293,37 @@ int main() {
   (void)hipMalloc(&d_clk, 16 * cus * 8);
   h_clk = (unsigned long long*)malloc(16 * cus * 8);
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d}\n", p.gcnArchName, cus, p.clockRate);
+  run64<0>(cus, 8, out, d_clk, h_clk);
+  run64<1>(cus, 8, out, d_clk, h_clk);
+  run64<2>(cus, 8, out, d_clk, h_clk);
+  run64<3>(cus, 8, out, d_clk, h_clk);
+  run64<4>(cus, 8, out, d_clk, h_clk);
+  if (getenv("PROBE_64_ONLY")) return 0;
+  for (int w : {8}) {
+    run_mix<0>(cus, w, out, d_clk, h_clk);
+    run_mix<4>(cus, w, out, d_clk, h_clk);
+    run_mix<5>(cus, w, out, d_clk, h_clk);
+    run_mix<1>(cus, w, out, d_clk, h_clk);
+    run_mix<2>(cus, w, out, d_clk, h_clk);
+    run_mix<3>(cus, w, out, d_clk, h_clk);
+    run_mix<6>(cus, w, out, d_clk, h_clk);
+    run_mix<7>(cus, w, out, d_clk, h_clk);
+    run_mix<8>(cus, w, out, d_clk, h_clk);
+    run_mix<9>(cus, w, out, d_clk, h_clk);
+  }
+  if (getenv("PROBE_MIX_ONLY")) return 0;
+  for (int w : {8}) {
+    run<14>(cus, w, out, d_clk, h_clk);
+    run<15>(cus, w, out, d_clk, h_clk);
+    run<16>(cus, w, out, d_clk, h_clk);
+    run<17>(cus, w, out, d_clk, h_clk);
+    run<18>(cus, w, out, d_clk, h_clk);
+    run<19>(cus, w, out, d_clk, h_clk);
+    run<20>(cus, w, out, d_clk, h_clk);
+    run<21>(cus, w, out, d_clk, h_clk);
+    run<22>(cus, w, out, d_clk, h_clk);
+  }
+  if (getenv("PROBE_NEW_ONLY")) return 0;
   for (int w : {8, 2, 1}) {
     run<0>(cus, w, out, d_clk, h_clk);
     run<1>(cus, w, out, d_clk, h_clk);
