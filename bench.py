@@ -138,7 +138,7 @@ def main():
     import torch
 
     dist = None
-    if world > 1:
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or os.environ.get("BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
@@ -192,6 +192,7 @@ def main():
         buf.free()
         dist.destroy_process_group()
         return
+    collective = "rccl all_reduce(min,sum) per step" if dist is not None else "none (single process)"
 
     kms = statistics.mean(kernel_ms) if kernel_ms else float("nan")
     value = world * WINDOW * args.steps / el
@@ -228,7 +229,7 @@ def main():
         "config": {"workload": "counter-nonce sweep of 2^32 nonces per GPU on fixed block S0, "
                                f"difficulty {d} bits (BASELINE config 2; config 4 when N>1)",
                    "template": "S0", "counters_per_gpu_per_step": WINDOW, "difficulty_bits": d,
-                   "parallelism": f"static nonce shards x{world}, RCCL all-reduce(min) per step"},
+                   "parallelism": f"static nonce shards x{world}; collective: {collective}"},
         "hashes_per_s_per_gpu": round(value / world, 1),
         "kernel_ms_per_step": round(kms, 3),
         "roofline": {"bound": "valu_int32", "achieved": round(achieved, 3), "peak": peak["nominal_tops"],
