@@ -79,6 +79,8 @@ typedef struct pow_stats {
 } pow_stats;
 
 /* ---- context --------------------------------------------------------- */
+/* Number of visible GPUs (HIP devices). */
+int pow_device_count(int* n);
 int pow_init(int device, pow_ctx** out);
 void pow_destroy(pow_ctx* ctx);
 const char* pow_last_error(void);

@@ -55,5 +55,40 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+MPI_HOME = os.environ.get("POW_MPI_HOME", "/opt/conda")  # the image's MPICH (mpi.h, libmpi.so)
+NODE_SRC = os.path.join(CSRC, "node", "pow_node.cpp")
+NODE_BIN = os.path.join(PKG, "bin", "pow_node")
+
+
+def mpi_available() -> bool:
+    return os.path.exists(os.path.join(MPI_HOME, "include", "mpi.h")) and \
+        os.path.exists(os.path.join(MPI_HOME, "lib", "libmpi.so"))
+
+
+def build_node(force: bool = False, verbose: bool = False) -> str | None:
+    """The protocol node (C++ + MPI) over libpow_gpu.so; skipped without MPI.
+    Run it with LD_LIBRARY_PATH=/lib/x86_64-linux-gnu:$MPI_HOME/lib (see
+    mpi_blockchain_amd/node.py): MPICH's directory also holds an older
+    libstdc++ that must not shadow the system one."""
+    if not mpi_available():
+        return None
+    build(force=False, verbose=verbose)
+    srcs = [NODE_SRC, LIB, os.path.join(ROOT, "include", "pow_gpu.h")]
+    if not force and os.path.exists(NODE_BIN) and \
+            all(os.path.getmtime(p) <= os.path.getmtime(NODE_BIN) for p in srcs):
+        return NODE_BIN
+    os.makedirs(os.path.dirname(NODE_BIN), exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O2", "-pthread", "-Wall", "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(MPI_HOME, "include"), NODE_SRC, "-o", NODE_BIN + ".tmp",
+           "-L", PKG, "-lpow_gpu", "-Wl,-rpath,$ORIGIN/..",
+           os.path.join(MPI_HOME, "lib", "libmpi.so"), f"-Wl,-rpath-link,{os.path.join(MPI_HOME, 'lib')}"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=ROOT)
+    os.replace(NODE_BIN + ".tmp", NODE_BIN)
+    return NODE_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_node(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,424 @@
+// pow_node — one MPI rank of the MPI_blockchain protocol with the gfx950 miner.
+//
+// Rebuilds the reference's node (node.cpp / blockchain.cpp) around the C ABI of
+// include/pow_gpu.h.  The protocol is kept as the reference defines it:
+//   * wire format: the MPI_BLOCK datatype of block.cpp:99-120 ({3 x MPI_INT @0,
+//     1 x MPI_UNSIGNED_LONG @16, 522 x MPI_UNSIGNED_CHAR @24}), tags 10/21/22
+//     (node.h:7-9) — reference CPU ranks and GPU ranks interoperate in one
+//     mpiexec (tests/test_node_gpu.py);
+//   * validation: valid_new_block (block.cpp:13-25) with the hash recomputed
+//     by the GPU (pow_hash_block) instead of picosha2;
+//   * fork resolution: the six cases of validate_block_for_chain
+//     (node.cpp:194-257), chain migration (node.cpp:152-191), chain service
+//     (node.cpp:334-359), broadcast in rotated order (node.cpp:260-273);
+//   * logging: the same stdout lines and <rank>.out chain dump (node.cpp:28-68);
+//   * termination: the first rank whose chain reaches BLOCKS_TO_MINE logs and
+//     calls MPI_Abort (node.cpp:286-290, 330).
+// What changes:
+//   * mining (node.cpp:292-308): each round refreshes the template exactly as
+//     node.cpp:292-299 and runs pow_mine over a counter range on this rank's
+//     GPU; the receive thread bumps a cancel epoch whenever the chain moves,
+//     which stops the round at its next sub-round boundary;
+//   * hardening: while waiting for a TAG_CHAIN_RESPONSE
+//     the receive thread keeps serving TAG_CHAIN_HASH requests and defers
+//     TAG_NEW_BLOCK messages, so two ranks asking each other cannot deadlock
+//     (node.cpp:161 blocks inside the mutex); the miner copies the last block
+//     under the mutex (node.cpp:292 reads it unlocked); a missing ancestor
+//     ends send_blockchain's walk instead of throwing (node.cpp:348).
+//
+//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS]
+#include <mpi.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <deque>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pow_gpu.h"
+
+namespace {
+
+// block.h:6-9, node.h:7-9
+constexpr int kValidationMinutes = 1;
+constexpr int kValidationBlocks = 5;
+constexpr int kTagNewBlock = 10;
+constexpr int kTagChainHash = 21;
+constexpr int kTagChainResponse = 22;
+
+struct Options {
+  unsigned difficulty = 9;  // DEFAULT_DIFFICULTY (block.h:6)
+  unsigned blocks = 10;     // BLOCKS_TO_MINE (block.h:7)
+  int device = -1;          // -1: local rank modulo visible GPUs
+  unsigned round_log2 = 32; // counters per pow_mine call
+  unsigned pause_ms = 0;    // sleep before each round (lets slower CPU ranks compete in tests)
+};
+
+std::string hash_of(const pow_block& b) { return std::string(b.block_hash); }
+std::string prev_of(const pow_block& b) { return std::string(b.previous_block_hash); }
+
+class Node {
+ public:
+  Node(const Options& o) : opt_(o) {}
+
+  int run();
+
+ private:
+  // ---- state (node.cpp:19-26) ----
+  Options opt_;
+  int rank_ = 0, size_ = 1;
+  std::map<std::string, pow_block> blocks_;  // node_blocks
+  const pow_block* last_ = nullptr;          // last_block_in_chain
+  pow_block genesis_{};
+  std::mutex mu_;                            // _sendMutex
+  uint32_t epoch_ = 0;                       // bumped whenever last_ moves
+  MPI_Datatype block_type_{};
+  pow_ctx* mine_ctx_ = nullptr;              // used only by the mining thread
+  pow_ctx* recv_ctx_ = nullptr;              // used only by the receive thread
+  std::deque<std::pair<pow_block, MPI_Status>> deferred_;
+
+  void bump_epoch() { __atomic_add_fetch(&epoch_, 1u, __ATOMIC_SEQ_CST); }
+  void set_last(const pow_block* b) {
+    last_ = b;
+    bump_epoch();
+  }
+
+  // block.cpp:99-120
+  void define_block_type() {
+    MPI_Aint disp[3] = {offsetof(pow_block, index), offsetof(pow_block, created_at),
+                        offsetof(pow_block, nonce)};
+    int len[3] = {3, 1, POW_NONCE_SIZE + POW_HASH_SIZE + POW_HASH_SIZE};
+    MPI_Datatype types[3] = {MPI_INT, MPI_UNSIGNED_LONG, MPI_UNSIGNED_CHAR};
+    if (MPI_Type_create_struct(3, len, disp, types, &block_type_) != MPI_SUCCESS ||
+        MPI_Type_commit(&block_type_) != MPI_SUCCESS) {
+      fprintf(stderr, "Error al crear el tipo\n");
+      MPI_Abort(MPI_COMM_WORLD, 1);
+    }
+  }
+
+  // block.cpp:74-77 through the GPU (K2) on the receive thread's context.
+  std::string gpu_hash(const pow_block& b) {
+    char hex[65];
+    if (pow_hash_block(recv_ctx_, &b, nullptr, hex) != POW_OK) {
+      fprintf(stderr, "[%d] pow_hash_block: %s\n", rank_, pow_last_error());
+      MPI_Abort(MPI_COMM_WORLD, 1);
+    }
+    return std::string(hex);
+  }
+
+  // block.cpp:13-25
+  bool valid_new_block(const pow_block& b) {
+    const unsigned long now = (unsigned long)time(nullptr);
+    bool valid = b.created_at + 60ul * kValidationMinutes >= now;
+    return valid && gpu_hash(b) == hash_of(b);
+  }
+
+  // node.cpp:111-115
+  bool check_first(const pow_block* chain, const pow_block& r) {
+    const std::string h = gpu_hash(chain[0]);
+    return chain[0].index == r.index && hash_of(chain[0]) == hash_of(r) && hash_of(chain[0]) == h;
+  }
+  // node.cpp:117-125
+  static bool check_chain(const pow_block* chain) {
+    bool ok = true;
+    for (int i = 0; i < kValidationBlocks - 1; ++i) {
+      if (prev_of(chain[i]).empty()) break;
+      ok = prev_of(chain[i]) == hash_of(chain[i + 1]) && chain[i].index - 1 == chain[i + 1].index && ok;
+    }
+    return ok;
+  }
+  // node.cpp:127-129
+  static bool equal(const pow_block& a, const pow_block& b) {
+    return a.index == b.index && a.node_owner_number == b.node_owner_number &&
+           a.difficulty == b.difficulty && a.created_at == b.created_at &&
+           std::string(a.nonce, strnlen(a.nonce, POW_NONCE_SIZE)) ==
+               std::string(b.nonce, strnlen(b.nonce, POW_NONCE_SIZE)) &&
+           prev_of(a) == prev_of(b) && hash_of(a) == hash_of(b);
+  }
+  // node.cpp:131-139: is `b` on my current chain?
+  bool look_for_block(const pow_block& b) {
+    const pow_block* cur = last_;
+    while (cur) {
+      if (equal(*cur, b)) return true;
+      const std::string p = prev_of(*cur);
+      if (p.empty()) break;
+      auto it = blocks_.find(p);
+      cur = it == blocks_.end() ? nullptr : &it->second;
+    }
+    return false;
+  }
+  // node.cpp:141-148
+  int find_block(const pow_block* chain) {
+    for (int i = 0; i < kValidationBlocks; ++i)
+      if (look_for_block(chain[i]) || chain[i].index == 1) return i;
+    return -1;
+  }
+
+  // node.cpp:334-359: up to VALIDATION_BLOCKS blocks back from the requested one.
+  void send_blockchain(pow_block from, int asker) {
+    std::vector<pow_block> chain(kValidationBlocks);
+    for (int i = 0; i < kValidationBlocks; ++i) {
+      chain[i] = from;
+      const std::string p = prev_of(from);
+      if (p.empty()) break;
+      auto it = blocks_.find(p);
+      if (it == blocks_.end()) break;  // the reference throws std::out_of_range here
+      from = it->second;
+    }
+    int rc = MPI_Send(chain.data(), kValidationBlocks, block_type_, asker, kTagChainResponse, MPI_COMM_WORLD);
+    if (rc != MPI_SUCCESS) printf("[%d] send to node %d failed with error code %d \n", rank_, asker, rc);
+  }
+
+  // node.cpp:152-191, with the wait made deadlock-free (see header).
+  bool verificar_y_migrar_cadena(const pow_block& r) {
+    const int owner = (int)r.node_owner_number;
+    MPI_Send(&r, 1, block_type_, owner, kTagChainHash, MPI_COMM_WORLD);
+    std::vector<pow_block> chain(kValidationBlocks);
+    for (;;) {
+      MPI_Status st;
+      MPI_Probe(MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, &st);
+      if (st.MPI_TAG == kTagChainResponse && st.MPI_SOURCE == owner) {
+        MPI_Recv(chain.data(), kValidationBlocks, block_type_, owner, kTagChainResponse, MPI_COMM_WORLD, &st);
+        break;
+      }
+      if (st.MPI_TAG == kTagChainResponse) {  // stale response from another rank: drop
+        std::vector<pow_block> junk(kValidationBlocks);
+        MPI_Recv(junk.data(), kValidationBlocks, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);
+        continue;
+      }
+      pow_block buf;
+      MPI_Recv(&buf, 1, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);
+      if (st.MPI_TAG == kTagChainHash) {
+        printf("[%u] TAG_CHAIN_HASH \n", rank_);
+        send_blockchain(buf, st.MPI_SOURCE);
+      } else if (st.MPI_TAG == kTagNewBlock) {
+        deferred_.emplace_back(buf, st);
+      }
+    }
+    const bool checks = check_first(chain.data(), r) && check_chain(chain.data());
+    const int i = find_block(chain.data());
+    printf("[%d]: find = %d | received_blockchain_checks = %d\n", rank_, i, checks ? 1 : 0);
+    if (checks && i > -1) {
+      for (int j = 0; j < i + 1; ++j) blocks_.insert({hash_of(chain[j]), chain[j]});
+      set_last(&blocks_.at(hash_of(chain[0])));
+      return true;
+    }
+    return false;
+  }
+
+  // node.cpp:194-257
+  bool validate_block_for_chain(const pow_block& r, const MPI_Status& st) {
+    if (valid_new_block(r)) {
+      blocks_.insert({hash_of(r), r});
+      const pow_block& last = *last_;
+      if (r.index == 1 && last.index == 0) {
+        set_last(&blocks_.at(hash_of(r)));
+        printf("[%d] Agregado a la lista bloque con index %u enviado por %d \n", rank_, r.index, st.MPI_SOURCE);
+        return true;
+      }
+      if (r.index == last.index + 1 && prev_of(r) == hash_of(last)) {
+        set_last(&blocks_.at(hash_of(r)));
+        printf("[%d] Agregado a la lista bloque con index %u enviado por %d \n", rank_, r.index, st.MPI_SOURCE);
+        return true;
+      }
+      if (r.index == last.index + 1 && prev_of(r) != hash_of(last)) {
+        printf("[%d] Perdí la carrera por uno (%d) contra %d \n", rank_, r.index, st.MPI_SOURCE);
+        return verificar_y_migrar_cadena(r);
+      }
+      if (r.index == last.index) {
+        printf("[%d] Conflicto suave: Conflicto de branch (%d) contra %d \n", rank_, r.index, st.MPI_SOURCE);
+        return false;
+      }
+      if (r.index < last.index) {
+        printf("[%d] Conflicto suave: Descarto el bloque (%d vs %d) contra %d \n", rank_, r.index, last.index,
+               st.MPI_SOURCE);
+        return false;
+      }
+      if (r.index > last.index + 1) {
+        printf("[%d] Perdí la carrera por varios contra %d \n", rank_, st.MPI_SOURCE);
+        return verificar_y_migrar_cadena(r);
+      }
+    }
+    printf("[%d] Error duro: Descarto el bloque recibido de %d porque no es válido \n", rank_, st.MPI_SOURCE);
+    return false;
+  }
+
+  // node.cpp:260-273
+  void send_block_to_everyone(const pow_block& b) {
+    for (int i = 1; i < size_; ++i) {
+      const int to = (rank_ + i) % size_;
+      int rc = MPI_Send(&b, 1, block_type_, to, kTagNewBlock, MPI_COMM_WORLD);
+      if (rc != MPI_SUCCESS) printf("[%d] send to node %d failed with error code %d \n", rank_, to, rc);
+    }
+  }
+
+  // node.cpp:40-68
+  void log_msg(const std::string& msg) {
+    std::ofstream out(std::to_string((unsigned long)rank_) + ".out", std::ios::app);
+    out << msg << "\n--------------------\n";
+  }
+  void log_chain(const std::string& info) {
+    std::ofstream out(std::to_string((unsigned long)rank_) + ".out", std::ios::app);
+    pow_block cur = *last_;
+    out << "Mi blockchain es la siguiente en " + info << "\n";
+    for (;;) {
+      out << "--------------------\n"
+          << "Block number: " << cur.index << "\n"
+          << "Owner: " << cur.node_owner_number << "\n"
+          << "Previous block hash: " << prev_of(cur) << "\n"
+          << "Block hash: " << hash_of(cur) << "\n"
+          << "--------------------\n";
+      const std::string p = prev_of(cur);
+      if (p.empty()) break;
+      auto it = blocks_.find(p);
+      if (it == blocks_.end()) break;
+      cur = it->second;
+    }
+  }
+
+  // node.cpp:278-332 with node.cpp:302-308 on the GPU.
+  void proof_of_work() {
+    std::mt19937_64 rng((uint64_t)time(nullptr) + (uint64_t)rank_);  // node.cpp:386
+    const uint64_t round = 1ull << opt_.round_log2;
+    for (;;) {
+      pow_block tmpl;
+      uint32_t ep;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (last_->index >= opt_.blocks) {  // node.cpp:286-290
+          log_msg("Terminé con la siguiente cadena");
+          log_chain("");
+          break;
+        }
+        tmpl = *last_;
+        ep = __atomic_load_n(&epoch_, __ATOMIC_SEQ_CST);
+      }
+      // node.cpp:295-299
+      tmpl.index += 1;
+      tmpl.node_owner_number = (uint32_t)rank_;
+      tmpl.difficulty = opt_.difficulty;
+      tmpl.created_at = (uint64_t)time(nullptr);
+      memcpy(tmpl.previous_block_hash, tmpl.block_hash, POW_HASH_SIZE);
+      if (opt_.pause_ms) std::this_thread::sleep_for(std::chrono::milliseconds(opt_.pause_ms));
+      const uint64_t start = rng() % (POW_COUNTER_LIMIT - round);
+      pow_block solved;
+      uint64_t ctr = 0;
+      int rc = pow_mine(mine_ctx_, &tmpl, start, round, opt_.difficulty, &epoch_, ep, &solved, &ctr, nullptr);
+      if (rc < 0) {
+        fprintf(stderr, "[%d] pow_mine: %s\n", rank_, pow_last_error());
+        MPI_Abort(MPI_COMM_WORLD, 1);
+      }
+      if (rc == 1) {  // node.cpp:311-327
+        std::lock_guard<std::mutex> g(mu_);
+        if (last_->index < solved.index) {
+          const std::string h = hash_of(solved);
+          blocks_.insert({h, solved});
+          set_last(&blocks_.at(h));
+          printf("[%d] Agregué un producido con index %u \n", rank_, last_->index);
+          send_block_to_everyone(*last_);
+        }
+      }
+    }
+    MPI_Abort(MPI_COMM_WORLD, 0);  // node.cpp:330
+  }
+};
+
+int Node::run() {
+  MPI_Comm_size(MPI_COMM_WORLD, &size_);
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank_);
+  define_block_type();
+  printf("[MPI] Lanzando proceso %u\n", rank_);
+  std::remove((std::to_string(rank_) + ".out").c_str());  // blockchain.cpp:31 does `rm *.out`
+
+  // one GPU per rank: node-local rank modulo the visible GPUs
+  int ndev = 1, local = rank_;
+  if (pow_device_count(&ndev) != POW_OK || ndev < 1) {
+    fprintf(stderr, "[%d] no GPU: %s\n", rank_, pow_last_error());
+    MPI_Abort(MPI_COMM_WORLD, 1);
+  }
+  for (const char* k : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK"})
+    if (const char* e = getenv(k)) { local = atoi(e); break; }
+  const int dev = opt_.device >= 0 ? opt_.device : local % ndev;
+  if (pow_init(dev, &mine_ctx_) != POW_OK || pow_init(dev, &recv_ctx_) != POW_OK) {
+    fprintf(stderr, "[%d] pow_init(%d): %s\n", rank_, dev, pow_last_error());
+    MPI_Abort(MPI_COMM_WORLD, 1);
+  }
+
+  // node.cpp:361-372
+  memset(&genesis_, 0, sizeof genesis_);
+  genesis_.index = 0;
+  genesis_.node_owner_number = (uint32_t)rank_;
+  genesis_.difficulty = opt_.difficulty;
+  genesis_.created_at = (uint64_t)time(nullptr);
+  last_ = &genesis_;
+
+  std::thread miner([this] { proof_of_work(); });
+  for (;;) {  // node.cpp:398-420
+    pow_block buf;
+    MPI_Status st;
+    if (!deferred_.empty()) {
+      buf = deferred_.front().first;
+      st = deferred_.front().second;
+      deferred_.pop_front();
+    } else {
+      MPI_Probe(MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, &st);
+      if (st.MPI_TAG == kTagChainResponse) {  // not waiting for one: drop it
+        std::vector<pow_block> junk(kValidationBlocks);
+        MPI_Recv(junk.data(), kValidationBlocks, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);
+        continue;
+      }
+      MPI_Recv(&buf, 1, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    if (st.MPI_TAG == kTagNewBlock) {
+      validate_block_for_chain(buf, st);
+    } else if (st.MPI_TAG == kTagChainHash) {
+      printf("[%u] TAG_CHAIN_HASH \n", rank_);
+      send_blockchain(buf, st.MPI_SOURCE);
+    }
+  }
+  miner.join();
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int provided = 0;
+  if (MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided) != MPI_SUCCESS) {
+    fprintf(stderr, "Error de MPI al inicializar.\n");
+    return 1;
+  }
+  if (provided < MPI_THREAD_MULTIPLE) {  // blockchain.cpp:15 never checks this
+    fprintf(stderr, "MPI_THREAD_MULTIPLE not provided (%d)\n", provided);
+    MPI_Abort(MPI_COMM_WORLD, 1);
+  }
+  setbuf(stdout, nullptr);  // blockchain.cpp:27-28
+  setbuf(stderr, nullptr);
+  Options o;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string k = argv[i];
+    const long v = strtol(argv[i + 1], nullptr, 10);
+    if (k == "--difficulty") o.difficulty = (unsigned)v;
+    else if (k == "--blocks") o.blocks = (unsigned)v;
+    else if (k == "--device") o.device = (int)v;
+    else if (k == "--round") o.round_log2 = (unsigned)std::min(40l, std::max(12l, v));
+    else if (k == "--pause-ms") o.pause_ms = (unsigned)v;
+  }
+  Node n(o);
+  n.run();
+  MPI_Finalize();
+  return 0;
+}

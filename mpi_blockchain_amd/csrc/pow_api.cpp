@@ -249,6 +249,13 @@ extern "C" {
 
 const char* pow_last_error(void) { return g_err.c_str(); }
 
+int pow_device_count(int* n) {
+  if (!n) return fail(POW_EINVAL, "null");
+  *n = 0;
+  HIP_OK(hipGetDeviceCount(n));
+  return POW_OK;
+}
+
 int pow_init(int device, pow_ctx** out) {
   if (!out) return fail(POW_EINVAL, "null out");
   *out = nullptr;

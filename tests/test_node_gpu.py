@@ -1,0 +1,60 @@
+"""Protocol runs (BASELINE config 5, scaled to one GPU): MPI networks of
+``pow_node`` ranks mining on the GPU through pow_mine, and mixed networks with
+the REFERENCE's own binary (oracle/_ref/blockchain_ref, built from
+/root/reference) — the reference's picosha2 validation (valid_new_block,
+block.cpp:13-25) accepting GPU-mined blocks is the wire-level parity check.
+"""
+import os
+
+import pytest
+
+from mpi_blockchain_amd.build import mpi_available
+from mpi_blockchain_amd.node import run_network
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not mpi_available(), reason="no MPI in this image")]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref")
+
+
+def leading_zero_bits(hexd: str) -> int:
+    return 256 - int(hexd, 16).bit_length()
+
+
+def check_chain(entries, blocks: int, difficulty: int):
+    """A logged chain (tip first): indices blocks..1, linked, every hash solving."""
+    assert [e.index for e in entries] == list(range(blocks, 0, -1))
+    for cur, prev in zip(entries, entries[1:]):
+        assert cur.prev == prev.hash
+    assert entries[-1].prev == ""  # block 1 points at the zeroed genesis hash
+    for e in entries:
+        assert len(e.hash) == 64 and leading_zero_bits(e.hash) >= difficulty
+
+
+@pytest.mark.parametrize("np_, d", [(4, 9), (6, 5)])
+def test_gpu_network(tmp_path, np_, d):
+    run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240)
+    assert run.returncode == 0, run.stdout[-3000:]
+    assert "Error duro" not in run.stdout
+    assert run.chains, run.stdout[-3000:]
+    for rank, entries in run.chains.items():
+        check_chain(entries, 10, d)
+    assert "Agregué un producido" in run.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference binary not built")
+def test_mixed_with_reference_nodes(tmp_path):
+    """2 reference ranks (picosha2, CPU) + 2 GPU ranks in one mpiexec at the
+    reference's DEFAULT_DIFFICULTY (9): the reference ranks validate and adopt
+    GPU-mined blocks, the GPU ranks validate the reference's."""
+    run = run_network(2, str(tmp_path), difficulty=9, blocks=10, timeout=240, ref_binary=REF_BIN, n_ref=2,
+                      extra_args=("--pause-ms", "30"))
+    assert run.returncode == 0, run.stdout[-3000:]
+    assert "Error duro" not in run.stdout, run.stdout[-3000:]
+    # reference ranks 0/1 accepted blocks sent by GPU ranks 2/3
+    import re
+
+    adopted = re.findall(r"\[(\d)\] Agregado a la lista bloque con index \d+ enviado por (\d)", run.stdout)
+    assert any(int(r) < 2 and int(s) >= 2 for r, s in adopted), run.stdout[-3000:]
+    for rank, entries in run.chains.items():
+        check_chain(entries, 10, 9)
