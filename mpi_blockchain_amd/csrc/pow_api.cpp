@@ -32,10 +32,14 @@ static_assert(offsetof(PowConsts, kw3) == 4 * PC_KW3, "PC_KW3");
 static_assert(offsetof(PowConsts, u18) == 4 * PC_U18, "PC_U18");
 static_assert(offsetof(PowConsts, w3) == 4 * PC_W3, "PC_W3");
 static_assert(offsetof(PowConsts, k) == 4 * PC_K, "PC_K");
+static_assert(offsetof(PowConsts, st0) == 4 * PC_ST0, "PC_ST0");
+static_assert(offsetof(PowConsts, w0raw) == 4 * PC_WRAW, "PC_WRAW");
 
 hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
                              const PowLaunch& L, uint32_t* out, PowResult* res);
 hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
+hipError_t pow_launch_search_lat(bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
+                                 const PowLaunchLat& L, PowResult* res);
 
 namespace {
 
@@ -140,6 +144,7 @@ void pow_build_consts(const pow_block* tmpl, PowConsts* C) {
   for (int k = 0; k < 6; ++k) C->u25[k] = ssig0(W[10 + k]) + W[9 + k];
   C->w15 = W[15];
   memcpy(C->k, kK, sizeof kK);
+  memcpy(C->w0raw, W, sizeof W);  // nonce words zero: W1 = W2 = 0, W3 = w3lo
   for (unsigned j = 0; j < POW_J; ++j) {
     const uint32_t w3 = ((uint32_t)(uint8_t)digit_char(j) << 24) | C->w3lo;
     C->w3[j] = w3;
@@ -165,6 +170,7 @@ struct pow_ctx {
   size_t hash_cap = 0;
   unsigned grid_full = 0;  // workgroups that fill the chip (8 per CU)
   bool force_full = false; // POW_FORCE_FULL=1: use the d > 32 kernel for every d (tests)
+  uint64_t lat_max = 1ull << 24;  // POW_LAT_MAX: first-sub-round cap for K1' (0 = K1 only)
   pow_stats stats{};
 };
 
@@ -236,6 +242,35 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   return POW_OK;
 }
 
+// One timed launch of the latency kernel K1' over [start, start+count), count <= 2^31.
+int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff) {
+  PowLaunchLat L;
+  memset(&L, 0, sizeof L);
+  uint64_t p = start;
+  for (int i = 8; i >= 0; --i) {
+    L.base_digit[i] = (uint32_t)(p % 62);
+    p /= 62;
+  }
+  L.count = count;
+  L.diff = diff;
+  L.thr = diff >= 32 ? 0u : (0xFFFFFFFFu >> diff);
+  PowResult init{};
+  init.min_rel = ~0ull;
+  HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, ctx->grid_full));
+  HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, grid, ctx->stream, ctx->d_consts, L, ctx->d_res));
+  HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
+  HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->stats.kernel_ms += ms;
+  ctx->stats.launches += 1;
+  ctx->stats.hashes += ctx->h_res->hashes;
+  return POW_OK;
+}
+
 int upload_consts(pow_ctx* ctx, const pow_block* tmpl) {
   PowConsts C;
   pow_build_consts(tmpl, &C);
@@ -275,6 +310,7 @@ int pow_init(int device, pow_ctx** out) {
   snprintf(ctx->name, sizeof ctx->name, "%s", prop.name);
   ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u;  // 8 x 256-thread WGs = 32 waves/CU
   if (const char* ff = getenv("POW_FORCE_FULL")) ctx->force_full = ff[0] == '1';
+  if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
   if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
     const int per = atoi(g);
     if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
@@ -480,17 +516,24 @@ int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t c
   ctx->stats = pow_stats{};
   if (hashes_done) *hashes_done = 0;
   if (int rc = upload_consts(ctx, tmpl)) return rc;
-  // Sub-rounds grow geometrically from ~4x the expected trials per solution
-  // (short time-to-block at low difficulty) to 2^30 counters (~0.1 s), the
-  // granularity at which the cancel word is polled.
+  // Sub-round 1 runs the latency kernel K1' over ~8x the expected trials per
+  // solution (capped at ctx->lat_max): it stops one wave-iteration after the
+  // first solution.  Later sub-rounds run the throughput kernel K1, growing
+  // 4x per round up to 2^30 counters (~0.13 s), the granularity at which the
+  // cancel word is polled.
   const unsigned dcap = diff_bits > 40 ? 40 : diff_bits;
-  uint64_t step = std::max<uint64_t>(62ull * 64, 1ull << std::min(dcap + 2, 30u));
+  uint64_t step = std::max<uint64_t>(1ull << 12, 1ull << std::min(dcap + 3, 40u));
   uint64_t done = 0;
+  bool first = true;
   while (done < ctr_count) {
     if (cancel_word && *cancel_word != epoch) break;
-    const uint64_t n = std::min(step, ctr_count - done);
+    const bool lat = first && ctx->lat_max > 0;
+    const uint64_t cap = lat ? ctx->lat_max : (uint64_t)1 << 30;
+    const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(step, cap), ctr_count - done);
     const uint64_t s0 = ctr_start + done;
-    if (int rc = run_search(ctx, s0, n, diff_bits, 1, nullptr, 0)) return rc;
+    if (int rc = lat ? run_search_lat(ctx, s0, n, diff_bits) : run_search(ctx, s0, n, diff_bits, 1, nullptr, 0))
+      return rc;
+    first = false;
     done += n;
     if (ctx->h_res->min_rel != ~0ull) {
       const uint64_t ctr = s0 + ctx->h_res->min_rel;
@@ -505,7 +548,7 @@ int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t c
       if (hashes_done) *hashes_done = ctx->stats.hashes;
       return 1;
     }
-    step = std::min<uint64_t>(step * 4, 1ull << 30);
+    step = std::min<uint64_t>(n * 4, 1ull << 30);
   }
   if (hashes_done) *hashes_done = ctx->stats.hashes;
   return 0;

@@ -113,7 +113,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
       long long lo = (long long)rbase * 62 - (long long)L.off0;
       if (lo > 0 && f < (unsigned long long)lo) break;
     }
-    ++iters;
     const uint32_t r = rbase + lane;
 
     // ---- per-prefix: nonce digits 0..7 = base digits + r (base 62) ----
@@ -148,6 +147,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     const uint32_t c32 = ssig0(W17) + W16;
 
     for (uint32_t j = 0; j < POW_J; ++j) {
+      if (MODE == 1 && j != 0 && (j & 7u) == 0) {
+        // Mid-chunk exit: this wave's remaining counters are all >= 62*rbase + j - off0.
+        unsigned long long f =
+            __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        f = uniform64(f);
+        long long lo = (long long)rbase * 62 + j - (long long)L.off0;
+        if (lo > 0 && f < (unsigned long long)lo) break;
+      }
+      ++iters;
       // ---------------- chunk 0, rounds 3..63 ----------------
       cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
       cptr J = pin(Cb, s2.a ^ j);  // per-j words and the chunk-0 uniform terms
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   if (MODE == 1) {
     // trials computed by this wave (lanes of a wave run the same iterations)
     if ((threadIdx.x & 63u) == 0)
-      atomicAdd(&res->hashes, (unsigned long long)iters * 64ull * POW_J);
+      atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);  // j-steps x lanes
   }
 }
 
@@ -241,6 +249,94 @@ template __global__ void pow_search<0, false>(const PowConsts*, PowLaunch, uint3
 template __global__ void pow_search<0, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
 template __global__ void pow_search<1, false>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
 template __global__ void pow_search<1, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+
+// K1' pow_search_lat<FULL> — latency form of the mining loop for short
+// ranges (the first sub-rounds of pow_mine).  One counter per lane; each wave
+// dequeues 64 CONSECUTIVE counters in increasing order, so the search can stop
+// one wave-iteration after the first solution (the lowest counter is final
+// once every lower dequeue has finished).  K1 instead keeps the lowest
+// prefixes' wave busy for all 62 values of the last digit (~0.6 ms on an idle
+// SIMD).  Costs ~8% more VALU per trial than K1 (no j-uniform terms).
+template <bool FULL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search_lat(
+    const PowConsts* __restrict__ C, PowLaunchLat L, PowResult* __restrict__ res) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t iters = 0;
+  cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
+  for (;;) {
+    uint32_t got = 0;
+    if (lane == 0) got = atomicAdd(&res->next, 64u);
+    const uint32_t q = __builtin_amdgcn_readfirstlane(got);
+    if ((unsigned long long)q >= L.count) break;
+    unsigned long long f =
+        __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (uniform64(f) < (unsigned long long)q) break;
+    ++iters;
+    const uint32_t rel = q + lane;
+    uint32_t dg[9];
+    {
+      uint32_t x = rel, carry = 0;
+#pragma unroll
+      for (int i = 8; i >= 0; --i) {
+        uint32_t qq = x / 62u;
+        uint32_t sm = L.base_digit[i] + (x - qq * 62u) + carry;
+        x = qq;
+        carry = sm >= 62u ? 1u : 0u;
+        dg[i] = carry ? sm - 62u : sm;
+      }
+    }
+    cptr P = pin(Cb, rel);
+    uint32_t w[64];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = P[PC_WRAW + i];
+    w[1] = (digit_char(dg[0]) << 24) | (digit_char(dg[1]) << 16) | (digit_char(dg[2]) << 8) | digit_char(dg[3]);
+    w[2] = (digit_char(dg[4]) << 24) | (digit_char(dg[5]) << 16) | (digit_char(dg[6]) << 8) | digit_char(dg[7]);
+    w[3] |= digit_char(dg[8]) << 24;  // [nonce[8], NUL, prev0, prev1]
+    St s{P[PC_ST0 + 0], P[PC_ST0 + 1], P[PC_ST0 + 2], P[PC_ST0 + 3],
+         P[PC_ST0 + 4], P[PC_ST0 + 5], P[PC_ST0 + 6], P[PC_ST0 + 7]};  // after round 0
+    round_k_w(s, P[PC_K + 1], w[1]);
+    round_k_w(s, P[PC_K + 2], w[2]);
+    round_k_w(s, P[PC_K + 3], w[3]);
+#pragma unroll
+    for (int i = 4; i < 16; ++i) round_kw(s, P[PC_KW0 + i]);
+    cptr Kp = pin(Cb + PC_K, s.e);
+#pragma unroll
+    for (int i = 16; i < 40; ++i) {
+      w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+      round_k_w(s, Kp[i], w[i]);
+    }
+    cptr K2 = pin(Cb + PC_K, s.e);
+#pragma unroll
+    for (int i = 40; i < 64; ++i) {
+      w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+      round_k_w(s, K2[i], w[i]);
+    }
+    uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
+                     IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+      const_chunk(t, as_const(C->kw[c]), H[0]);
+      H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
+      H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
+    }
+    St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+    const_chunk(t, as_const(C->kw[3]), H[0]);
+    const uint32_t h0 = H[0] + t.a;
+    bool hit = h0 <= L.thr;
+    if (FULL && hit) {
+      uint32_t D[8] = {h0, H[1] + t.b, H[2] + t.c, H[3] + t.d,
+                       H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
+      hit = full_test(D, L.diff);
+    }
+    if (__builtin_expect(hit, 0) && (unsigned long long)rel < L.count)
+      atomicMin(&res->min_rel, (unsigned long long)rel);
+  }
+  if (lane == 0) atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);
+}
+
+template __global__ void pow_search_lat<false>(const PowConsts*, PowLaunchLat, PowResult*);
+template __global__ void pow_search_lat<true>(const PowConsts*, PowLaunchLat, PowResult*);
 
 // K2: block_to_hash for n blocks; `msgs` holds each block's 270-byte message
 // already padded on the host to 320 bytes (80 big-endian words).
@@ -271,6 +367,14 @@ extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hi
   else if (mode == 0) hipLaunchKernelGGL((pow_search<0, true>), g, b, 0, stream, C, L, out, res);
   else if (!full) hipLaunchKernelGGL((pow_search<1, false>), g, b, 0, stream, C, L, out, res);
   else hipLaunchKernelGGL((pow_search<1, true>), g, b, 0, stream, C, L, out, res);
+  return hipGetLastError();
+}
+
+extern "C++" hipError_t pow_launch_search_lat(bool full, unsigned grid, hipStream_t stream,
+                                              const PowConsts* C, const PowLaunchLat& L, PowResult* res) {
+  dim3 g(grid), b(256);
+  if (!full) hipLaunchKernelGGL((pow_search_lat<false>), g, b, 0, stream, C, L, res);
+  else hipLaunchKernelGGL((pow_search_lat<true>), g, b, 0, stream, C, L, res);
   return hipGetLastError();
 }
 

@@ -42,18 +42,30 @@ struct PowConsts {
   uint32_t u18[POW_J];   // s0(W3(j)) + W11          -> W18 = s1(W16) + W2 + u18[j]
   uint32_t w3[POW_J];    // W3(j)                      -> W19
   uint32_t k[64];        // K[0..63] (streamed from memory: VOP3 takes no literal)
+  uint32_t w0raw[16];    // chunk-0 words as hashed (W1..W3 = 0 placeholders; latency kernel)
 };
 
 // Word offsets into PowConsts for the kernel's constant-address-space loads.
-#define PC_KW0 (256 + 8)
+#define PC_ST0 256
+#define PC_KW0 (PC_ST0 + 8)
 #define PC_U20 (PC_KW0 + 16 + 4 + 3)
 #define PC_U25 (PC_U20 + 5)
 #define PC_KW3 (PC_U25 + 6 + 4)
 #define PC_U18 (PC_KW3 + POW_J)
 #define PC_W3 (PC_U18 + POW_J)
 #define PC_K (PC_W3 + POW_J)
+#define PC_WRAW (PC_K + 64)
 
 // Launch parameters of one kernel dispatch.
+// Launch parameters of the latency kernel (one counter per lane).
+struct PowLaunchLat {
+  uint32_t base_digit[9];  // base-62 digits of ctr_start (nonce[0..8])
+  uint32_t thr;            // as PowLaunch
+  uint32_t diff;
+  uint32_t pad;
+  uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
+};
+
 struct PowLaunch {
   uint32_t base_digit[8];  // base-62 digits of the first prefix P0 (nonce[0..7])
   uint32_t n_prefix;       // prefixes P0 .. P0 + n_prefix - 1

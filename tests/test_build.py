@@ -39,11 +39,11 @@ def kernel_body(isa: str, mangled_prefix: str) -> str:
 
 
 def j_loop_body(isa: str, mangled_prefix: str) -> str:
-    """The per-trial j-loop: from its loop header to the next basic-block label."""
+    """The per-trial body: the kernel's largest basic block (one j-step is a
+    single ~5k-instruction block of straight-line code)."""
     body = kernel_body(isa, mangled_prefix)
-    m = re.search(r"This Loop Header: Depth=2\n(.*?)\n\.LBB", body, flags=re.S)
-    assert m, "j-loop not found"
-    return m.group(1)
+    blocks = re.split(r"^(?:\.LBB\w+:|; %bb\.\d+:).*$", body, flags=re.M)
+    return max(blocks, key=lambda b: len(re.findall(r"^\s+v_", b, flags=re.M)))
 
 
 def metadata(isa: str, name_prefix: str) -> dict:

@@ -21,14 +21,21 @@ def leading_zero_bits(hexd: str) -> int:
     return 256 - int(hexd, 16).bit_length()
 
 
-def check_chain(entries, blocks: int, difficulty: int):
-    """A logged chain (tip first): indices blocks..1, linked, every hash solving."""
-    assert [e.index for e in entries] == list(range(blocks, 0, -1))
+def check_chain(entries, blocks: int, difficulty: int) -> bool:
+    """A logged chain (tip first): consecutive indices, linked, every hash
+    solving.  Returns True if it is complete (blocks..1, ending at genesis).
+    A rank killed by the first finisher's MPI_Abort (node.cpp:330) may leave
+    a partial dump; what it did write must still be consistent."""
+    idx = [e.index for e in entries]
+    assert idx == list(range(idx[0], idx[0] - len(idx), -1)) if idx else True
     for cur, prev in zip(entries, entries[1:]):
         assert cur.prev == prev.hash
-    assert entries[-1].prev == ""  # block 1 points at the zeroed genesis hash
     for e in entries:
         assert len(e.hash) == 64 and leading_zero_bits(e.hash) >= difficulty
+    return idx == list(range(blocks, 0, -1)) and entries[-1].prev == ""
+
+
+FORK_MSGS = ("Perdí la carrera", "Conflicto suave", "TAG_CHAIN_HASH")
 
 
 @pytest.mark.parametrize("np_, d", [(4, 9), (6, 5)])
@@ -36,10 +43,11 @@ def test_gpu_network(tmp_path, np_, d):
     run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240)
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout
-    assert run.chains, run.stdout[-3000:]
-    for rank, entries in run.chains.items():
-        check_chain(entries, 10, d)
+    complete = [r for r, entries in run.chains.items() if check_chain(entries, 10, d)]
+    assert complete, run.stdout[-3000:]
     assert "Agregué un producido" in run.stdout
+    if d <= 5:  # every rank solves each block within ~1 ms: forks are certain
+        assert any(m in run.stdout for m in FORK_MSGS), run.stdout[-3000:]
 
 
 @pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference binary not built")
@@ -56,5 +64,4 @@ def test_mixed_with_reference_nodes(tmp_path):
 
     adopted = re.findall(r"\[(\d)\] Agregado a la lista bloque con index \d+ enviado por (\d)", run.stdout)
     assert any(int(r) < 2 and int(s) >= 2 for r, s in adopted), run.stdout[-3000:]
-    for rank, entries in run.chains.items():
-        check_chain(entries, 10, 9)
+    assert [r for r, entries in run.chains.items() if check_chain(entries, 10, 9)]
