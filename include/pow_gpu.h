@@ -125,6 +125,15 @@ int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t c
              unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
              pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
 
+/* Lowest-latency form of pow_mine: returns (1) SOME solving counter of the
+ * range — the first one the GPU finds; every wave stops at its next step —
+ * instead of the lowest.  Same arguments, outputs and return codes.  Not
+ * deterministic (like the reference's rand() nonces, node.cpp:302); use it
+ * where only time-to-block matters (the protocol node, the difficulty ladder). */
+int pow_mine_any(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                 unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+                 pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
+
 /* Deterministic parity / throughput mode: every solving counter of
  * [ctr_start, ctr_start + ctr_count) (ctr_count <= 2^32), written to out_ctrs
  * as (counter - ctr_start), ascending.  *n_found = number of solutions

@@ -87,6 +87,8 @@ def load() -> ctypes.CDLL:
         "pow_hash_block": ([ctypes.c_void_p, P, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
         "pow_mine": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
                       ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
+        "pow_mine_any": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                          ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
         "pow_sweep": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
                        ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, c_sizep], ctypes.c_int),
         "pow_sweep_device": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
@@ -107,7 +109,7 @@ def load() -> ctypes.CDLL:
 
 EXPORTS = ("pow_device_count", "pow_init", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
-           "pow_hash_block", "pow_mine", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
+           "pow_hash_block", "pow_mine", "pow_mine_any", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak")
 
 

@@ -73,6 +73,7 @@ class Node {
  public:
   Node(const Options& o) : opt_(o) {}
 
+  int init_gpu();
   int run();
 
  private:
@@ -315,9 +316,10 @@ class Node {
       const uint64_t start = rng() % (POW_COUNTER_LIMIT - round);
       pow_block solved;
       uint64_t ctr = 0;
-      int rc = pow_mine(mine_ctx_, &tmpl, start, round, opt_.difficulty, &epoch_, ep, &solved, &ctr, nullptr);
+      // first solution found in the range: the reference's random nonces have no order either
+      int rc = pow_mine_any(mine_ctx_, &tmpl, start, round, opt_.difficulty, &epoch_, ep, &solved, &ctr, nullptr);
       if (rc < 0) {
-        fprintf(stderr, "[%d] pow_mine: %s\n", rank_, pow_last_error());
+        fprintf(stderr, "[%d] pow_mine_any: %s\n", rank_, pow_last_error());
         MPI_Abort(MPI_COMM_WORLD, 1);
       }
       if (rc == 1) {  // node.cpp:311-327
@@ -335,26 +337,33 @@ class Node {
   }
 };
 
+// GPU setup runs BEFORE MPI_Init: HIP start-up takes ~1 s, and MPICH's
+// MPI_Init synchronises every process of the job (reference ranks included),
+// so no rank starts mining while a GPU rank is still initialising.  The
+// device is the node-local rank (from the launcher's environment) modulo the
+// visible GPUs.
+int Node::init_gpu() {
+  int ndev = 0, local = 0;
+  if (pow_device_count(&ndev) != POW_OK || ndev < 1) {
+    fprintf(stderr, "no GPU: %s\n", pow_last_error());
+    return 1;
+  }
+  for (const char* k : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "PMI_RANK"})
+    if (const char* e = getenv(k)) { local = atoi(e); break; }
+  const int dev = opt_.device >= 0 ? opt_.device : local % ndev;
+  if (pow_init(dev, &mine_ctx_) != POW_OK || pow_init(dev, &recv_ctx_) != POW_OK) {
+    fprintf(stderr, "pow_init(%d): %s\n", dev, pow_last_error());
+    return 1;
+  }
+  return 0;
+}
+
 int Node::run() {
   MPI_Comm_size(MPI_COMM_WORLD, &size_);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank_);
   define_block_type();
   printf("[MPI] Lanzando proceso %u\n", rank_);
   std::remove((std::to_string(rank_) + ".out").c_str());  // blockchain.cpp:31 does `rm *.out`
-
-  // one GPU per rank: node-local rank modulo the visible GPUs
-  int ndev = 1, local = rank_;
-  if (pow_device_count(&ndev) != POW_OK || ndev < 1) {
-    fprintf(stderr, "[%d] no GPU: %s\n", rank_, pow_last_error());
-    MPI_Abort(MPI_COMM_WORLD, 1);
-  }
-  for (const char* k : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK"})
-    if (const char* e = getenv(k)) { local = atoi(e); break; }
-  const int dev = opt_.device >= 0 ? opt_.device : local % ndev;
-  if (pow_init(dev, &mine_ctx_) != POW_OK || pow_init(dev, &recv_ctx_) != POW_OK) {
-    fprintf(stderr, "[%d] pow_init(%d): %s\n", rank_, dev, pow_last_error());
-    MPI_Abort(MPI_COMM_WORLD, 1);
-  }
 
   // node.cpp:361-372
   memset(&genesis_, 0, sizeof genesis_);
@@ -396,17 +405,6 @@ int Node::run() {
 }  // namespace
 
 int main(int argc, char** argv) {
-  int provided = 0;
-  if (MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided) != MPI_SUCCESS) {
-    fprintf(stderr, "Error de MPI al inicializar.\n");
-    return 1;
-  }
-  if (provided < MPI_THREAD_MULTIPLE) {  // blockchain.cpp:15 never checks this
-    fprintf(stderr, "MPI_THREAD_MULTIPLE not provided (%d)\n", provided);
-    MPI_Abort(MPI_COMM_WORLD, 1);
-  }
-  setbuf(stdout, nullptr);  // blockchain.cpp:27-28
-  setbuf(stderr, nullptr);
   Options o;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i];
@@ -418,6 +416,18 @@ int main(int argc, char** argv) {
     else if (k == "--pause-ms") o.pause_ms = (unsigned)v;
   }
   Node n(o);
+  if (n.init_gpu() != 0) return 1;
+  int provided = 0;
+  if (MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided) != MPI_SUCCESS) {
+    fprintf(stderr, "Error de MPI al inicializar.\n");
+    return 1;
+  }
+  if (provided < MPI_THREAD_MULTIPLE) {  // blockchain.cpp:15 never checks this
+    fprintf(stderr, "MPI_THREAD_MULTIPLE not provided (%d)\n", provided);
+    MPI_Abort(MPI_COMM_WORLD, 1);
+  }
+  setbuf(stdout, nullptr);  // blockchain.cpp:27-28
+  setbuf(stderr, nullptr);
   n.run();
   MPI_Finalize();
   return 0;

@@ -38,7 +38,7 @@ static_assert(offsetof(PowConsts, w0raw) == 4 * PC_WRAW, "PC_WRAW");
 hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
                              const PowLaunch& L, uint32_t* out, PowResult* res);
 hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
-hipError_t pow_launch_search_lat(bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
+hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConsts* C,
                                  const PowLaunchLat& L, PowResult* res);
 
 namespace {
@@ -238,12 +238,12 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats.kernel_ms += ms;
   ctx->stats.launches += 1;
-  ctx->stats.hashes += mode == 1 ? ctx->h_res->hashes : (uint64_t)L.n_prefix * POW_J;
+  ctx->stats.hashes += mode >= 1 ? ctx->h_res->hashes : (uint64_t)L.n_prefix * POW_J;
   return POW_OK;
 }
 
 // One timed launch of the latency kernel K1' over [start, start+count), count <= 2^31.
-int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff) {
+int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, bool any) {
   PowLaunchLat L;
   memset(&L, 0, sizeof L);
   uint64_t p = start;
@@ -259,7 +259,8 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff) 
   HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, ctx->grid_full));
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
-  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, grid, ctx->stream, ctx->d_consts, L, ctx->d_res));
+  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->d_consts, L,
+                               ctx->d_res));
   HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -507,9 +508,13 @@ int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t 
   return n > cap ? fail(POW_ENOSPC, "%zu solutions > cap %zu", n, cap) : POW_OK;
 }
 
-int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
-             unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
-             pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
+// pow_mine (any = false: lowest solving counter, deterministic) and
+// pow_mine_any (any = true: the first solution any wave finds; the whole grid
+// stops at its next step — the reference's random-nonce miner has no order
+// either, node.cpp:302).
+static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                     unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+                     pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done, bool any) {
   if (!ctx || !out) return fail(POW_EINVAL, "null");
   if (int rc = check_range(tmpl, ctr_start, ctr_count, diff_bits)) return rc;
   if (int rc = set_dev(ctx)) return rc;
@@ -531,7 +536,8 @@ int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t c
     const uint64_t cap = lat ? ctx->lat_max : (uint64_t)1 << 30;
     const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(step, cap), ctr_count - done);
     const uint64_t s0 = ctr_start + done;
-    if (int rc = lat ? run_search_lat(ctx, s0, n, diff_bits) : run_search(ctx, s0, n, diff_bits, 1, nullptr, 0))
+    if (int rc = lat ? run_search_lat(ctx, s0, n, diff_bits, any)
+                     : run_search(ctx, s0, n, diff_bits, any ? 2 : 1, nullptr, 0))
       return rc;
     first = false;
     done += n;
@@ -552,6 +558,20 @@ int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t c
   }
   if (hashes_done) *hashes_done = ctx->stats.hashes;
   return 0;
+}
+
+int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+             unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+             pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
+  return mine_impl(ctx, tmpl, ctr_start, ctr_count, diff_bits, cancel_word, epoch, out, found_ctr,
+                   hashes_done, false);
+}
+
+int pow_mine_any(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                 unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+                 pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
+  return mine_impl(ctx, tmpl, ctr_start, ctr_count, diff_bits, cancel_word, epoch, out, found_ctr,
+                   hashes_done, true);
 }
 
 int pow_dev_alloc(pow_ctx* ctx, size_t bytes, void** out) {

@@ -105,12 +105,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     if (lane == 0) got = atomicAdd(&res->next, 64u);
     const uint32_t rbase = __builtin_amdgcn_readfirstlane(got);
     if (rbase >= L.n_prefix) break;
-    if (MODE == 1) {
-      // Early exit: every counter of this and later chunks is >= 62*rbase - off0.
+    if (MODE >= 1) {
+      // Early exit.  MODE 1: every counter of this and later chunks is
+      // >= 62*rbase - off0.  MODE 2 (first found): any solution ends the search.
       unsigned long long f =
           __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       f = uniform64(f);
       long long lo = (long long)rbase * 62 - (long long)L.off0;
+      if (MODE == 2 && f != ~0ull) break;
       if (lo > 0 && f < (unsigned long long)lo) break;
     }
     const uint32_t r = rbase + lane;
@@ -146,14 +148,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     const uint32_t c31 = ssig0(W16) + C->w15;
     const uint32_t c32 = ssig0(W17) + W16;
 
+    bool stop = false;
     for (uint32_t j = 0; j < POW_J; ++j) {
-      if (MODE == 1 && j != 0 && (j & 7u) == 0) {
+      if (MODE == 1 && j != 0 && (j & 1u) == 0) {
         // Mid-chunk exit: this wave's remaining counters are all >= 62*rbase + j - off0.
         unsigned long long f =
             __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         f = uniform64(f);
         long long lo = (long long)rbase * 62 + j - (long long)L.off0;
         if (lo > 0 && f < (unsigned long long)lo) break;
+      }
+      if (MODE == 2 && j != 0) {
+        unsigned long long f =
+            __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (uniform64(f) != ~0ull) {
+          stop = true;
+          break;
+        }
       }
       ++iters;
       // ---------------- chunk 0, rounds 3..63 ----------------
@@ -237,8 +248,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         }
       }
     }
+    if (MODE == 2 && stop) break;
   }
-  if (MODE == 1) {
+  if (MODE >= 1) {
     // trials computed by this wave (lanes of a wave run the same iterations)
     if ((threadIdx.x & 63u) == 0)
       atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);  // j-steps x lanes
@@ -249,6 +261,8 @@ template __global__ void pow_search<0, false>(const PowConsts*, PowLaunch, uint3
 template __global__ void pow_search<0, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
 template __global__ void pow_search<1, false>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
 template __global__ void pow_search<1, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+template __global__ void pow_search<2, false>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
+template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
 
 // K1' pow_search_lat<FULL> — latency form of the mining loop for short
 // ranges (the first sub-rounds of pow_mine).  One counter per lane; each wave
@@ -257,7 +271,7 @@ template __global__ void pow_search<1, true>(const PowConsts*, PowLaunch, uint32
 // once every lower dequeue has finished).  K1 instead keeps the lowest
 // prefixes' wave busy for all 62 values of the last digit (~0.6 ms on an idle
 // SIMD).  Costs ~8% more VALU per trial than K1 (no j-uniform terms).
-template <bool FULL>
+template <bool FULL, bool ANY>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search_lat(
     const PowConsts* __restrict__ C, PowLaunchLat L, PowResult* __restrict__ res) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -270,7 +284,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     if ((unsigned long long)q >= L.count) break;
     unsigned long long f =
         __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (uniform64(f) < (unsigned long long)q) break;
+    f = uniform64(f);
+    if (ANY ? f != ~0ull : f < (unsigned long long)q) break;
     ++iters;
     const uint32_t rel = q + lane;
     uint32_t dg[9];
@@ -335,8 +350,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   if (lane == 0) atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);
 }
 
-template __global__ void pow_search_lat<false>(const PowConsts*, PowLaunchLat, PowResult*);
-template __global__ void pow_search_lat<true>(const PowConsts*, PowLaunchLat, PowResult*);
+template __global__ void pow_search_lat<false, false>(const PowConsts*, PowLaunchLat, PowResult*);
+template __global__ void pow_search_lat<true, false>(const PowConsts*, PowLaunchLat, PowResult*);
+template __global__ void pow_search_lat<false, true>(const PowConsts*, PowLaunchLat, PowResult*);
+template __global__ void pow_search_lat<true, true>(const PowConsts*, PowLaunchLat, PowResult*);
 
 // K2: block_to_hash for n blocks; `msgs` holds each block's 270-byte message
 // already padded on the host to 320 bytes (80 big-endian words).
@@ -365,16 +382,20 @@ extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hi
   dim3 g(grid), b(256);
   if (mode == 0 && !full) hipLaunchKernelGGL((pow_search<0, false>), g, b, 0, stream, C, L, out, res);
   else if (mode == 0) hipLaunchKernelGGL((pow_search<0, true>), g, b, 0, stream, C, L, out, res);
-  else if (!full) hipLaunchKernelGGL((pow_search<1, false>), g, b, 0, stream, C, L, out, res);
-  else hipLaunchKernelGGL((pow_search<1, true>), g, b, 0, stream, C, L, out, res);
+  else if (mode == 1 && !full) hipLaunchKernelGGL((pow_search<1, false>), g, b, 0, stream, C, L, out, res);
+  else if (mode == 1) hipLaunchKernelGGL((pow_search<1, true>), g, b, 0, stream, C, L, out, res);
+  else if (!full) hipLaunchKernelGGL((pow_search<2, false>), g, b, 0, stream, C, L, out, res);
+  else hipLaunchKernelGGL((pow_search<2, true>), g, b, 0, stream, C, L, out, res);
   return hipGetLastError();
 }
 
-extern "C++" hipError_t pow_launch_search_lat(bool full, unsigned grid, hipStream_t stream,
+extern "C++" hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream,
                                               const PowConsts* C, const PowLaunchLat& L, PowResult* res) {
   dim3 g(grid), b(256);
-  if (!full) hipLaunchKernelGGL((pow_search_lat<false>), g, b, 0, stream, C, L, res);
-  else hipLaunchKernelGGL((pow_search_lat<true>), g, b, 0, stream, C, L, res);
+  if (!full && !any) hipLaunchKernelGGL((pow_search_lat<false, false>), g, b, 0, stream, C, L, res);
+  else if (!any) hipLaunchKernelGGL((pow_search_lat<true, false>), g, b, 0, stream, C, L, res);
+  else if (!full) hipLaunchKernelGGL((pow_search_lat<false, true>), g, b, 0, stream, C, L, res);
+  else hipLaunchKernelGGL((pow_search_lat<true, true>), g, b, 0, stream, C, L, res);
   return hipGetLastError();
 }
 

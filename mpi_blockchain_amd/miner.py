@@ -107,14 +107,16 @@ class GpuMiner:
         return self._cancel.value
 
     def mine(self, tmpl: Block, start: int = 0, count: int = 1 << 40, difficulty: int = DEFAULT_DIFFICULTY,
-             epoch: int | None = None) -> MineResult | None:
-        """Lowest solving counter in [start, start+count); None if none / cancelled."""
+             epoch: int | None = None, any_solution: bool = False) -> MineResult | None:
+        """Lowest solving counter in [start, start+count) (pow_mine), or the
+        first one found (pow_mine_any, lowest latency); None if none / cancelled."""
         out = Block()
         ctr, hashes = ctypes.c_uint64(), ctypes.c_uint64()
         ep = self._cancel.value if epoch is None else epoch
-        rc = check(self.L.pow_mine(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
-                                   ctypes.byref(self._cancel), ep, ctypes.byref(out),
-                                   ctypes.byref(ctr), ctypes.byref(hashes)))
+        fn = self.L.pow_mine_any if any_solution else self.L.pow_mine
+        rc = check(fn(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
+                      ctypes.byref(self._cancel), ep, ctypes.byref(out),
+                      ctypes.byref(ctr), ctypes.byref(hashes)))
         if rc == 0:
             return None
         return MineResult(out, ctr.value, hashes.value, self.stats()["kernel_ms"])

@@ -42,6 +42,23 @@ def miner_full():
     m.close()
 
 
+@pytest.fixture(scope="module")
+def miner_k1():
+    """pow_mine on the throughput kernel only (latency kernel K1' disabled)."""
+    os.environ["POW_LAT_MAX"] = "0"
+    try:
+        m = GpuMiner(0)
+    finally:
+        os.environ.pop("POW_LAT_MAX", None)
+    yield m
+    m.close()
+
+
+@pytest.fixture(params=["lat+k1", "k1"])
+def mminer(request, miner, miner_k1):
+    return miner if request.param == "lat+k1" else miner_k1
+
+
 def test_device_is_gfx950(miner):
     info = miner.device_info()
     assert info["cu_count"] > 0
@@ -97,13 +114,13 @@ def test_sweep_count_and_min(miner, golden, templates):
             assert mn == first
 
 
-def test_mine_lowest_counter(miner, golden, templates):
+def test_mine_lowest_counter(mminer, golden, templates):
     """pow_mine returns the LOWEST solving counter and a block the reference
     would accept (nonce + strcpy'd hex, node.cpp:318)."""
     for w in golden["windows"]:
         b = block_from_template(templates[w["template"]])
         for d, s in w["sets"].items():
-            r = miner.mine(b, w["start"], w["count"], int(d))
+            r = mminer.mine(b, w["start"], w["count"], int(d))
             if s["count"] == 0:
                 assert r is None
                 continue
@@ -111,13 +128,13 @@ def test_mine_lowest_counter(miner, golden, templates):
             assert r.counter == w["start"] + s["counters"][0]
             assert field(r.block, "nonce") == nonce_from_counter(r.counter)
             hx = block_hex(r.block)
-            assert hx == miner.block_to_hash(r.block)
+            assert hx == mminer.block_to_hash(r.block)
             assert field(r.block, "block_hash")[64] == 0
             assert field(r.block, "block_hash")[65:] == field(b, "block_hash")[65:]
             assert r.hashes >= r.counter - w["start"]
 
 
-def test_mine_from_every_offset(miner, golden, templates):
+def test_mine_from_every_offset(mminer, golden, templates):
     """Start the search inside a prefix (off0 = 1..61) just before a known solution."""
     w = golden["windows"][0]  # S0 [0, 2^20)
     b = block_from_template(templates[w["template"]])
@@ -126,8 +143,28 @@ def test_mine_from_every_offset(miner, golden, templates):
         target = sol[k]
         prev = sol[k - 1] + 1 if k else 0
         start = max(prev, target - (k % 62))
-        r = miner.mine(b, start, 4096, 9)
+        r = mminer.mine(b, start, 4096, 9)
         assert r is not None and r.counter == target
+
+
+def test_mine_any_returns_a_solution(mminer, golden, templates):
+    """pow_mine_any: some solving counter of the range (a member of the golden
+    set), None when the range holds none."""
+    for w in golden["windows"]:
+        b = block_from_template(templates[w["template"]])
+        for d, s in w["sets"].items():
+            r = mminer.mine(b, w["start"], w["count"], int(d), any_solution=True)
+            if s["count"] == 0:
+                assert r is None
+                continue
+            assert r is not None
+            rel = r.counter - w["start"]
+            assert 0 <= rel < w["count"]
+            if s["count"] <= 4096:
+                assert rel in set(s["counters"])
+            hx = block_hex(r.block)
+            assert hx == mminer.block_to_hash(r.block)
+            assert 256 - int(hx, 16).bit_length() >= int(d)
 
 
 def test_mine_no_solution_and_bounds(miner, templates):

@@ -56,7 +56,7 @@ def test_mixed_with_reference_nodes(tmp_path):
     reference's DEFAULT_DIFFICULTY (9): the reference ranks validate and adopt
     GPU-mined blocks, the GPU ranks validate the reference's."""
     run = run_network(2, str(tmp_path), difficulty=9, blocks=10, timeout=240, ref_binary=REF_BIN, n_ref=2,
-                      extra_args=("--pause-ms", "30"))
+                      extra_args=("--pause-ms", "5"))
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout, run.stdout[-3000:]
     # reference ranks 0/1 accepted blocks sent by GPU ranks 2/3
@@ -64,4 +64,6 @@ def test_mixed_with_reference_nodes(tmp_path):
 
     adopted = re.findall(r"\[(\d)\] Agregado a la lista bloque con index \d+ enviado por (\d)", run.stdout)
     assert any(int(r) < 2 and int(s) >= 2 for r, s in adopted), run.stdout[-3000:]
+    # and GPU ranks accepted blocks mined by the reference (validated by K2)
+    assert any(int(r) >= 2 and int(s) < 2 for r, s in adopted), run.stdout[-3000:]
     assert [r for r, entries in run.chains.items() if check_chain(entries, 10, 9)]
