@@ -243,7 +243,8 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
 }
 
 // One timed launch of the latency kernel K1' over [start, start+count), count <= 2^31.
-int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, bool any) {
+int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, bool any,
+                   unsigned waves_per_simd) {
   PowLaunchLat L;
   memset(&L, 0, sizeof L);
   uint64_t p = start;
@@ -257,7 +258,9 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   PowResult init{};
   init.min_rel = ~0ull;
   HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
-  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, ctx->grid_full));
+  // A 256-thread workgroup puts one wave on each SIMD of its CU.
+  const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->d_consts, L,
                                ctx->d_res));
@@ -521,22 +524,30 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   ctx->stats = pow_stats{};
   if (hashes_done) *hashes_done = 0;
   if (int rc = upload_consts(ctx, tmpl)) return rc;
-  // Sub-round 1 runs the latency kernel K1' over ~8x the expected trials per
-  // solution (capped at ctx->lat_max): it stops one wave-iteration after the
-  // first solution.  Later sub-rounds run the throughput kernel K1, growing
-  // 4x per round up to 2^30 counters (~0.13 s), the granularity at which the
-  // cancel word is polled.
+  // Sub-round plan.
+  //  * d <= 21 (expected trials <= 2M): sub-round 1 on the latency kernel K1'
+  //    over 16x the expected trials, capped at ctx->lat_max.  Few waves per
+  //    SIMD: a wave-iteration (64 trials per lane-set) then takes ~10 us
+  //    instead of ~66 us at 8 waves/SIMD, which sets the time to first hit.
+  //  * then the throughput kernel K1.  pow_mine_any: single 2^30-counter
+  //    launches (~0.13 s, the cancel-poll granularity); every wave stops
+  //    within one j-step of the first hit.  pow_mine (lowest counter): waves
+  //    holding lower counters must finish, so sub-rounds start near the
+  //    expected trials and grow 4x.
   const unsigned dcap = diff_bits > 40 ? 40 : diff_bits;
-  uint64_t step = std::max<uint64_t>(1ull << 12, 1ull << std::min(dcap + 3, 40u));
+  const bool use_lat = ctx->lat_max > 0 && diff_bits <= 21;
+  const unsigned lat_wps = diff_bits <= 17 ? 1 : diff_bits <= 19 ? 2 : 4;
+  uint64_t step = use_lat ? std::max<uint64_t>(1ull << 12, 1ull << (dcap + 4))
+                          : (any ? 1ull << 30 : std::max<uint64_t>(1ull << 12, 1ull << std::min(dcap + 2, 30u)));
   uint64_t done = 0;
   bool first = true;
   while (done < ctr_count) {
     if (cancel_word && *cancel_word != epoch) break;
-    const bool lat = first && ctx->lat_max > 0;
+    const bool lat = first && use_lat;
     const uint64_t cap = lat ? ctx->lat_max : (uint64_t)1 << 30;
     const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(step, cap), ctr_count - done);
     const uint64_t s0 = ctr_start + done;
-    if (int rc = lat ? run_search_lat(ctx, s0, n, diff_bits, any)
+    if (int rc = lat ? run_search_lat(ctx, s0, n, diff_bits, any, lat_wps)
                      : run_search(ctx, s0, n, diff_bits, any ? 2 : 1, nullptr, 0))
       return rc;
     first = false;
@@ -554,7 +565,7 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
       if (hashes_done) *hashes_done = ctx->stats.hashes;
       return 1;
     }
-    step = std::min<uint64_t>(n * 4, 1ull << 30);
+    step = any ? 1ull << 30 : std::min<uint64_t>(n * 4, 1ull << 30);
   }
   if (hashes_done) *hashes_done = ctx->stats.hashes;
   return 0;

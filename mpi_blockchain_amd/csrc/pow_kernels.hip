@@ -265,23 +265,26 @@ template __global__ void pow_search<2, false>(const PowConsts*, PowLaunch, uint3
 template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32_t*, PowResult*);
 
 // K1' pow_search_lat<FULL> — latency form of the mining loop for short
-// ranges (the first sub-rounds of pow_mine).  One counter per lane; each wave
-// dequeues 64 CONSECUTIVE counters in increasing order, so the search can stop
-// one wave-iteration after the first solution (the lowest counter is final
-// once every lower dequeue has finished).  K1 instead keeps the lowest
+// ranges (the first sub-rounds of pow_mine).  One counter per lane; in
+// iteration k, wave w of W takes the 64 CONSECUTIVE counters starting at
+// 64*(k*W + w), so the grid sweeps the range in increasing order and the
+// search can stop one wave-iteration after the first solution (the lowest
+// counter is final once every lower iteration has finished).  The assignment
+// is static: with thousands of waves a shared atomic queue head (~88 dequeues
+// per us) would itself bound the rate.  K1 instead keeps the lowest
 // prefixes' wave busy for all 62 values of the last digit (~0.6 ms on an idle
 // SIMD).  Costs ~8% more VALU per trial than K1 (no j-uniform terms).
 template <bool FULL, bool ANY>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search_lat(
     const PowConsts* __restrict__ C, PowLaunchLat L, PowResult* __restrict__ res) {
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * 4u;
   uint32_t iters = 0;
   cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
-  for (;;) {
-    uint32_t got = 0;
-    if (lane == 0) got = atomicAdd(&res->next, 64u);
-    const uint32_t q = __builtin_amdgcn_readfirstlane(got);
-    if ((unsigned long long)q >= L.count) break;
+  for (unsigned long long qq = (unsigned long long)wave * 64u; qq < L.count;
+       qq += (unsigned long long)nwaves * 64u) {
+    const uint32_t q = (uint32_t)qq;
     unsigned long long f =
         __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     f = uniform64(f);
