@@ -87,6 +87,16 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
         return {"error": str(e)}
 
 
+def pmc_traffic():
+    """HBM bytes per dispatch of this workload from the committed rocprofv3
+    PMC summary (tools/profile_round.sh + tools/pmc_summary.py)."""
+    p = os.path.join(ROOT, "profiles", "r01", "final", "pmc_summary.json")
+    try:
+        return int(json.load(open(p))["hbm_bytes_per_dispatch"]["total"])
+    except Exception:
+        return None
+
+
 def ladder(miner, n_templates: int = 101, rungs=(9, 13, 17, 21, 25)) -> dict:
     """BASELINE config 3: time-to-block (median over templates, seed 1) and
     sustained hashes/s per difficulty rung.  Time-to-block uses pow_mine_any
@@ -235,9 +245,12 @@ def main():
         "hashes_per_s_per_gpu": round(value / world, 1),
         "kernel_ms_per_step": round(kms, 3),
         "roofline": {"bound": "valu_int32", "achieved": round(achieved, 3), "peak": peak["nominal_tops"],
-                     "unit": "Tops/s", "frac": round(achieved / peak["nominal_tops"], 4), "traffic": None,
+                     "unit": "Tops/s", "frac": round(achieved / peak["nominal_tops"], 4),
+                     "traffic": pmc_traffic(), "algorithmic_bytes": 4 * (last[0] or 0),
                      "ops_per_hash": OPS_PER_HASH, "peak_detail": peak,
-                     "note": "achieved = 2^32 hashes x 5000 int32 ops / mean HIP-event kernel time"},
+                     "note": ("achieved = 2^32 hashes x 5000 int32 ops / mean HIP-event kernel time; "
+                              "traffic = FETCH_SIZE+WRITE_SIZE bytes per dispatch of the same workload "
+                              "(profiles/r01/final/pmc_summary.json, separate rocprofv3 --pmc passes)")},
         "device": info,
         "parity": parity,
     }

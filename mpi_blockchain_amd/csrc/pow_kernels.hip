@@ -72,6 +72,17 @@ __device__ __forceinline__ void const_chunk(St& t, cptr kwbase, uint32_t dep) {
   }
 }
 
+// Append a wave's staged solutions (n <= 128, in LDS) to the global list with
+// one atomic: lanes store consecutive entries (coalesced).
+__device__ __forceinline__ void flush_stage(const uint32_t* wst, uint32_t n, uint32_t lane,
+                                            PowResult* res, uint32_t* out, uint32_t cap) {
+  uint32_t got = 0;
+  if (lane == 0) got = atomicAdd(&res->count, n);
+  const uint32_t base = __builtin_amdgcn_readfirstlane(got);
+  for (uint32_t i = lane; i < n; i += 64u)
+    if (base + i < cap) out[base + i] = wst[i];
+}
+
 // Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
 __device__ __forceinline__ bool full_test(const uint32_t H[8], uint32_t d) {
   uint32_t lz = 0;
@@ -99,6 +110,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     PowResult* __restrict__ res) {
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t iters = 0;
+  // Sweep mode: solutions are staged per wave in LDS and flushed in batches
+  // (one atomic + coalesced stores per >= 64 solutions); the lowest solution
+  // is kept per lane and min-reduced once per wave at exit.  One atomic per
+  // solution would make every solution a separate memory-side request
+  // (~0.68 GB of requests per 2^32 sweep at d = 9 for 34 MB of data).
+  __shared__ uint32_t stage[4][128];
+  uint32_t* wst = stage[threadIdx.x >> 6];
+  uint32_t nst = 0;                     // staged entries (wave-uniform)
+  unsigned long long mymin = ~0ull;     // lowest solution of this lane
 
   for (;;) {
     uint32_t got = 0;
@@ -237,18 +257,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
                          H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
         hit = full_test(D, L.diff);
       }
-      if (__builtin_expect(hit, 0)) {
-        const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
-        if (rel < L.count) {  // also rejects j < off0 at r = 0 (wraps) and lanes past the end
-          atomicMin(&res->min_rel, rel);
-          if (MODE == 0) {
-            uint32_t idx = atomicAdd(&res->count, 1u);
-            if (idx < L.cap) out[idx] = (uint32_t)rel;
+      if (MODE != 0) {
+        if (__builtin_expect(hit, 0)) {
+          const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
+          // rel < count also rejects j < off0 at r = 0 (wraps) and lanes past the end
+          if (rel < L.count) atomicMin(&res->min_rel, rel);
+        }
+      } else {
+        bool ok = false;
+        uint32_t relv = 0;
+        if (__builtin_expect(hit, 0)) {
+          const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
+          ok = rel < L.count;
+          relv = (uint32_t)rel;
+          if (ok && rel < mymin) mymin = rel;
+        }
+        const unsigned long long m = __ballot(ok);
+        if (m) {  // wave-uniform
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (ok) wst[nst + rank] = relv;
+          nst += (uint32_t)__popcll(m);
+          if (nst >= 64) {
+            flush_stage(wst, nst, lane, res, out, L.cap);
+            nst = 0;
           }
         }
       }
     }
     if (MODE == 2 && stop) break;
+  }
+  if (MODE == 0) {
+    if (nst) flush_stage(wst, nst, lane, res, out, L.cap);
+    // wave min of the per-lane minima, one atomic per wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(mymin, off, 64);
+      mymin = o < mymin ? o : mymin;
+    }
+    if (lane == 0 && mymin != ~0ull) atomicMin(&res->min_rel, mymin);
   }
   if (MODE >= 1) {
     // trials computed by this wave (lanes of a wave run the same iterations)
