@@ -97,6 +97,40 @@ def pmc_traffic():
         return None
 
 
+def protocol_runs() -> dict:
+    """BASELINE config 1 (the reference: mpiexec -np 4 ./blockchain, 10 blocks
+    at DEFAULT_DIFFICULTY = 9, picosha2 on CPU) beside config 5 scaled to this
+    GPU (4 pow_node ranks, same protocol, GPU mining): wall time to a
+    10-block chain, process start-up included."""
+    import tempfile
+
+    out = {}
+    try:
+        from mpi_blockchain_amd.build import mpi_available
+        from mpi_blockchain_amd.node import MPIEXEC, mpi_env, run_network
+
+        if not mpi_available():
+            return {"skipped": "no MPI"}
+        ref = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref")
+        if os.path.exists(ref):
+            with tempfile.TemporaryDirectory() as td:
+                t = time.perf_counter()
+                p = subprocess.run(["timeout", "-k", "5", "120", MPIEXEC, "-np", "4", ref], cwd=td,
+                                   env=mpi_env(), capture_output=True, text=True)
+                out["reference_np4_d9_wall_s"] = round(time.perf_counter() - t, 3)
+                out["reference_rc"] = p.returncode
+        for d in (9, 25):
+            with tempfile.TemporaryDirectory() as td:
+                t = time.perf_counter()
+                run = run_network(4, td, difficulty=d, blocks=10, timeout=180)
+                out[f"gpu_np4_d{d}_wall_s"] = round(time.perf_counter() - t, 3)
+                out[f"gpu_np4_d{d}_rc"] = run.returncode
+                out[f"gpu_np4_d{d}_chains"] = len(run.chains)
+    except Exception as e:  # pragma: no cover
+        out["error"] = str(e)
+    return out
+
+
 def ladder(miner, n_templates: int = 101, rungs=(9, 13, 17, 21, 25)) -> dict:
     """BASELINE config 3: time-to-block (median over templates, seed 1) and
     sustained hashes/s per difficulty rung.  Time-to-block uses pow_mine_any
@@ -142,6 +176,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ladder", action="store_true")
     ap.add_argument("--no-peak", action="store_true")
+    ap.add_argument("--no-protocol", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -258,6 +293,8 @@ def main():
         res["cpu_baseline"] = cpu_baseline()
     if world == 1 and not args.no_ladder:
         res["ladder"] = ladder(miner)
+    if world == 1 and not args.no_protocol:
+        res["protocol"] = protocol_runs()
     buf.free()
     print(json.dumps(res), flush=True)
     if dist is not None:
