@@ -83,6 +83,9 @@ typedef struct pow_stats {
 int pow_device_count(int* n);
 int pow_init(int device, pow_ctx** out);
 void pow_destroy(pow_ctx* ctx);
+/* Launch every kernel once with empty work so the code objects are loaded and
+ * the first real call pays no start-up cost (HIP loads them lazily). */
+int pow_warmup(pow_ctx* ctx);
 const char* pow_last_error(void);
 int pow_get_stats(const pow_ctx* ctx, pow_stats* out);
 /* Device properties the roofline uses: CU count and peak engine clock (kHz). */

@@ -75,6 +75,7 @@ def load() -> ctypes.CDLL:
         "pow_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "pow_init": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "pow_destroy": ([ctypes.c_void_p], None),
+        "pow_warmup": ([ctypes.c_void_p], ctypes.c_int),
         "pow_last_error": ([], ctypes.c_char_p),
         "pow_get_stats": ([ctypes.c_void_p, ctypes.POINTER(PowStats)], ctypes.c_int),
         "pow_device_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
@@ -107,7 +108,7 @@ def load() -> ctypes.CDLL:
     return L
 
 
-EXPORTS = ("pow_device_count", "pow_init", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
+EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak")

@@ -351,7 +351,8 @@ int Node::init_gpu() {
   for (const char* k : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "PMI_RANK"})
     if (const char* e = getenv(k)) { local = atoi(e); break; }
   const int dev = opt_.device >= 0 ? opt_.device : local % ndev;
-  if (pow_init(dev, &mine_ctx_) != POW_OK || pow_init(dev, &recv_ctx_) != POW_OK) {
+  if (pow_init(dev, &mine_ctx_) != POW_OK || pow_init(dev, &recv_ctx_) != POW_OK ||
+      pow_warmup(mine_ctx_) != POW_OK || pow_warmup(recv_ctx_) != POW_OK) {
     fprintf(stderr, "pow_init(%d): %s\n", dev, pow_last_error());
     return 1;
   }

@@ -353,6 +353,26 @@ void pow_destroy(pow_ctx* ctx) {
   delete ctx;
 }
 
+int pow_warmup(pow_ctx* ctx) {
+  if (!ctx) return fail(POW_EINVAL, "null");
+  if (int rc = set_dev(ctx)) return rc;
+  PowLaunch L;
+  memset(&L, 0, sizeof L);  // n_prefix = 0: every wave exits at its first dequeue
+  PowLaunchLat LL;
+  memset(&LL, 0, sizeof LL);  // count = 0
+  for (int mode = 0; mode < 3; ++mode)
+    for (int full = 0; full < 2; ++full)
+      HIP_OK(pow_launch_search(mode, full != 0, 1, ctx->stream, ctx->d_consts, L, nullptr, ctx->d_res));
+  for (int any = 0; any < 2; ++any)
+    for (int full = 0; full < 2; ++full)
+      HIP_OK(pow_launch_search_lat(full != 0, any != 0, 1, ctx->stream, ctx->d_consts, LL, ctx->d_res));
+  HIP_OK(pow_launch_hash(0, ctx->stream, nullptr, nullptr));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  pow_block b;
+  memset(&b, 0, sizeof b);
+  return pow_hash_blocks(ctx, &b, 1, nullptr, nullptr);
+}
+
 int pow_get_stats(const pow_ctx* ctx, pow_stats* out) {
   if (!ctx || !out) return fail(POW_EINVAL, "null");
   *out = ctx->stats;

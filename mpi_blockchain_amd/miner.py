@@ -48,6 +48,10 @@ class GpuMiner:
         self.device = device
         self._cancel = ctypes.c_uint32(0)
 
+    def warmup(self) -> None:
+        """Load every kernel now (HIP loads code objects at first launch)."""
+        check(self.L.pow_warmup(self.ctx))
+
     # ---- lifecycle ----
     def close(self) -> None:
         if self.ctx:
