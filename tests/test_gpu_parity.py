@@ -230,3 +230,29 @@ def test_full_window_2p32(miner, fingerprints, templates):
         n, mn = miner.sweep_count(b, 0, 1 << 32, int(d))
         assert n == lad[d]["count"]
         assert mn == lad[d]["first"][0]
+
+
+def test_random_templates_vs_oracle(miner):
+    """Fresh random templates (arbitrary header fields, binary or hex-string
+    prev hashes, random window starts): GPU sweep == C-oracle sweep."""
+    import random
+
+    from mpi_blockchain_amd.block import make_block
+    from oracle.oracle import Oracle, make_oblock
+
+    O = Oracle()
+    rng = random.Random(424242)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    for k in range(12):
+        idx, own, dif, cat = (rng.randrange(1 << 32), rng.randrange(1 << 32), rng.randrange(1 << 32),
+                              rng.randrange(1 << 64))
+        if k % 2:
+            prev = bytes(rng.randrange(256) for _ in range(256))
+        else:
+            prev = hashlib.sha256(bytes([k])).hexdigest().encode()
+        start = rng.randrange(62**9 - (1 << 20))
+        count = rng.randrange(1 << 16, 1 << 18)
+        d = rng.choice([6, 8, 10])
+        got = miner.sweep(make_block(idx, own, dif, cat, prev), start, count, d)
+        want, n = O.sweep(make_oblock(idx, own, dif, cat, prev), start, count, d, cap=count, threads=threads)
+        assert got.tolist() == want.tolist(), (k, start, count, d)
