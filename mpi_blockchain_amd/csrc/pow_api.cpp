@@ -38,6 +38,8 @@ static_assert(offsetof(PowConsts, w0raw) == 4 * PC_WRAW, "PC_WRAW");
 hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
                              const PowLaunch& L, uint32_t* out, PowResult* res);
 hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
+hipError_t pow_sort_u32(void* temp, size_t* temp_bytes, uint32_t* keys, uint32_t* alt, uint32_t n,
+                        uint32_t** sorted, hipStream_t stream);
 hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConsts* C,
                                  const PowLaunchLat& L, PowResult* res);
 
@@ -163,7 +165,10 @@ struct pow_ctx {
   PowConsts* d_consts = nullptr;
   PowResult* d_res = nullptr;
   PowResult* h_res = nullptr;  // pinned
-  uint32_t* d_out = nullptr;
+  uint32_t* d_out = nullptr;   // pow_sweep's device list and its radix-sort twin
+  uint32_t* d_alt = nullptr;
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   size_t out_cap = 0;
   uint32_t* d_msgs = nullptr;
   uint32_t* d_dig = nullptr;
@@ -344,6 +349,8 @@ void pow_destroy(pow_ctx* ctx) {
   (void)hipFree(ctx->d_consts);
   (void)hipFree(ctx->d_res);
   (void)hipFree(ctx->d_out);
+  (void)hipFree(ctx->d_alt);
+  (void)hipFree(ctx->d_sort_tmp);
   (void)hipFree(ctx->d_msgs);
   (void)hipFree(ctx->d_dig);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
@@ -510,11 +517,20 @@ int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t 
   if (!ctx || !n_found) return fail(POW_EINVAL, "null");
   if (cap && !out_ctrs) return fail(POW_EINVAL, "cap without buffer");
   if (int rc = set_dev(ctx)) return rc;
+  if (cap > 0xFFFFFFFFu) cap = 0xFFFFFFFFu;
   if (cap > ctx->out_cap) {
     (void)hipFree(ctx->d_out);
-    ctx->d_out = nullptr;
-    ctx->out_cap = 0;
+    (void)hipFree(ctx->d_alt);
+    (void)hipFree(ctx->d_sort_tmp);
+    ctx->d_out = ctx->d_alt = nullptr;
+    ctx->d_sort_tmp = nullptr;
+    ctx->out_cap = ctx->sort_tmp_bytes = 0;
     HIP_OK(hipMalloc(&ctx->d_out, cap * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&ctx->d_alt, cap * sizeof(uint32_t)));
+    size_t tb = 0;
+    HIP_OK(pow_sort_u32(nullptr, &tb, ctx->d_out, ctx->d_alt, (uint32_t)cap, nullptr, ctx->stream));
+    HIP_OK(hipMalloc(&ctx->d_sort_tmp, tb ? tb : 1));
+    ctx->sort_tmp_bytes = tb;
     ctx->out_cap = cap;
   }
   size_t n = 0;
@@ -525,8 +541,12 @@ int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t 
   *n_found = n;
   const size_t got = std::min(n, cap);
   if (got) {
-    HIP_OK(hipMemcpy(out_ctrs, ctx->d_out, got * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    std::sort(out_ctrs, out_ctrs + got);
+    // ascending order: device radix sort (the kernel appends in completion order)
+    uint32_t* sorted = ctx->d_out;
+    size_t tb = ctx->sort_tmp_bytes;
+    HIP_OK(pow_sort_u32(ctx->d_sort_tmp, &tb, ctx->d_out, ctx->d_alt, (uint32_t)got, &sorted, ctx->stream));
+    HIP_OK(hipMemcpyAsync(out_ctrs, sorted, got * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
   }
   return n > cap ? fail(POW_ENOSPC, "%zu solutions > cap %zu", n, cap) : POW_OK;
 }
