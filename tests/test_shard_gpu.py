@@ -1,0 +1,45 @@
+"""ShardedMiner on the GPU: pow_mine per shard + the torch.distributed
+all-reduce(min) (gloo here, world size 1; RCCL in bench.py) returns the same
+counter as one un-sharded pow_mine."""
+import os
+import socket
+
+import pytest
+
+from mpi_blockchain_amd.block import make_block
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sharded_equals_unsharded():
+    import torch.distributed as dist
+
+    from mpi_blockchain_amd.miner import GpuMiner
+    from mpi_blockchain_amd.shard import ShardedMiner, sharded_mine
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with GpuMiner(0) as m:
+            b = make_block(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
+            sm = ShardedMiner(m, 0, 1)
+            for d in (9, 13, 17):
+                want = m.mine(b, 0, 1 << 24, d)
+                got = sm.mine(b, 0, 1 << 24, d, round_size=1 << 20)
+                assert want is not None and got == want.counter
+            # 3 simulated ranks over the same range, each mining its shard on the GPU
+            def search(start, n):
+                r = m.mine(b, start, n, 13)
+                return None if r is None else r.counter
+            from mpi_blockchain_amd.shard import NONE, partition
+            best = NONE
+            for rank in range(3):
+                v = sharded_mine(search, lambda x: x, 0, 1 << 20, 1 << 20, rank, 3)
+                best = min(best, NONE if v is None else v)
+            assert best == m.mine(b, 0, 1 << 20, 13).counter
+    finally:
+        dist.destroy_process_group()
