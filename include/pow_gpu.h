@@ -69,6 +69,7 @@ enum {
   POW_ENOSPC = -2,    /* pow_sweep: more solutions than `cap` */
   POW_EHIP = -3,      /* a HIP runtime call failed; see pow_last_error() */
   POW_ENODEV = -4,    /* no such GPU */
+  POW_ECOMM = -5,     /* RCCL unavailable or a collective failed (pow_group_*) */
 };
 
 /* Per-call statistics of the last pow_mine / pow_sweep / pow_hash_blocks. */
@@ -159,6 +160,40 @@ int pow_dev_alloc(pow_ctx* ctx, size_t bytes, void** out);
 int pow_dev_free(pow_ctx* ctx, void* p);
 /* Copy `bytes` from a device pointer to host memory (synchronous). */
 int pow_dev_read(pow_ctx* ctx, const void* dev, void* host, size_t bytes);
+
+/* ---- sharded search over several GPUs (RCCL) --------------------------- */
+/* One template mined cooperatively by `nranks` GPUs, one pow_ctx each (one
+ * process or host thread per GPU).  The reference has no such mode: its ranks
+ * compete, each on its own template (node.cpp:302, 386).  These calls are
+ * collective: every rank makes them with the same arguments.  RCCL is loaded
+ * on first use (dlopen); without it they return POW_ECOMM. */
+#define POW_GROUP_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+enum { POW_REDUCE_MIN = 0, POW_REDUCE_MAX = 1, POW_REDUCE_SUM = 2 };
+typedef struct pow_group pow_group;
+
+/* Rank `rank`'s contiguous static shard of [start, start + count): shards of
+ * ranks 0..nranks-1 are consecutive and differ in size by at most one. */
+void pow_group_partition(uint64_t start, uint64_t count, int rank, int nranks,
+                         uint64_t* shard_start, uint64_t* shard_count);
+/* Rank 0 makes the id; the caller hands it to every rank (MPI_Bcast, a file,
+ * torch.distributed ...) before pow_group_init. */
+int pow_group_unique_id(uint8_t id[POW_GROUP_ID_BYTES]);
+/* Joins the RCCL communicator on ctx's GPU; returns once all ranks joined. */
+int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
+                   pow_group** out);
+void pow_group_destroy(pow_group* g);
+/* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream. */
+int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);
+/* pow_mine over all ranks: rounds of `round_size` counters (0 = 2^30 per
+ * rank), each split into static shards; each rank mines the lowest solving
+ * counter of its shard, then one 24-byte ncclAllReduce(ncclMin) per round
+ * picks the winner, spreads cancellation (any rank whose cancel word moved
+ * stops every rank: returns 0) and failures (every rank returns < 0).  On 1 the
+ * result equals pow_mine's over the whole range on one GPU, on every rank:
+ * *out / *found_ctr as pow_mine; *hashes_done = this rank's trials. */
+int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                   uint64_t round_size, unsigned diff_bits, const volatile uint32_t* cancel_word,
+                   uint32_t epoch, pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
 
 #ifdef __cplusplus
 }

@@ -17,9 +17,11 @@ NONCE_SIZE = 10
 MSG_BYTES = 270
 COUNTER_LIMIT = 62**9
 
-POW_OK, POW_EINVAL, POW_ENOSPC, POW_EHIP, POW_ENODEV = 0, -1, -2, -3, -4
+POW_OK, POW_EINVAL, POW_ENOSPC, POW_EHIP, POW_ENODEV, POW_ECOMM = 0, -1, -2, -3, -4, -5
 _ERRNAMES = {POW_EINVAL: "POW_EINVAL", POW_ENOSPC: "POW_ENOSPC", POW_EHIP: "POW_EHIP",
-             POW_ENODEV: "POW_ENODEV"}
+             POW_ENODEV: "POW_ENODEV", POW_ECOMM: "POW_ECOMM"}
+GROUP_ID_BYTES = 128
+POW_REDUCE_MIN, POW_REDUCE_MAX, POW_REDUCE_SUM = 0, 1, 2
 
 
 class PowError(RuntimeError):
@@ -97,6 +99,15 @@ def load() -> ctypes.CDLL:
         "pow_dev_alloc": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "pow_dev_free": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
         "pow_dev_read": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+        "pow_group_partition": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, c_u64p, c_u64p],
+                                None),
+        "pow_group_unique_id": ([ctypes.c_char_p], ctypes.c_int),
+        "pow_group_init": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                            ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "pow_group_destroy": ([ctypes.c_void_p], None),
+        "pow_group_allreduce_u64": ([ctypes.c_void_p, c_u64p, ctypes.c_size_t, ctypes.c_int], ctypes.c_int),
+        "pow_group_mine": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                            ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
         "pow_valu_peak": ([ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
                           ctypes.c_int),
     }
@@ -111,7 +122,8 @@ def load() -> ctypes.CDLL:
 EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
-           "pow_dev_read", "pow_valu_peak")
+           "pow_dev_read", "pow_valu_peak", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
+           "pow_group_destroy", "pow_group_allreduce_u64", "pow_group_mine")
 
 
 def check(rc: int) -> int:

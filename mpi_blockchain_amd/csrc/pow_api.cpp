@@ -289,6 +289,10 @@ int upload_consts(pow_ctx* ctx, const pow_block* tmpl) {
 
 }  // namespace
 
+int pow_ctx_device(const pow_ctx* ctx) { return ctx->device; }
+void* pow_ctx_stream(const pow_ctx* ctx) { return (void*)ctx->stream; }
+int pow_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
 extern "C" {
 
 const char* pow_last_error(void) { return g_err.c_str(); }

@@ -1,0 +1,236 @@
+// Sharded multi-GPU search over RCCL (BASELINE config 4).
+//
+// One pow_ctx per GPU, one process (or host thread) per GPU.  A search of
+// [start, start + count) runs in rounds of `round_size` counters.  Each round
+// is cut into `nranks` contiguous static shards (pow_group_partition, the same
+// split as mpi_blockchain_amd/shard.py); every rank runs pow_mine (lowest
+// solving counter) on its shard, then ONE ncclAllReduce(ncclUint64, ncclMin)
+// of three words {lowest counter, go, ok} picks the winner, carries
+// cancellation and reports a failed peer.  Every rank returns the same
+// counter: the one a single GPU (or the CPU oracle) finds first.
+//
+// The reference has no mining-side collective: each MPI rank mines its own
+// template with its own rand() stream (node.cpp:302, 386) and talks only on
+// success (send_block_to_everyone, node.cpp:260-273).  This is the
+// cooperative form of that search: one template, several GPUs.
+//
+// RCCL is opened with dlopen at first use, so libpow_gpu.so has no link-time
+// dependency on it and the single-GPU entry points never load it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/pow_gpu.h"
+#include "pow_template.h"
+
+namespace {
+
+// The RCCL entry points used here (rccl.h:187, 220, 260, 339, 611).
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  char why[256] = {0};  // non-empty: RCCL is unusable
+};
+
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!h) {
+      snprintf(x.why, sizeof x.why, "cannot load RCCL: %s", dlerror());
+      return x;
+    }
+    x.get_unique_id = (decltype(x.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    x.comm_init_rank = (decltype(x.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+    x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
+    x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+    if (!x.get_unique_id || !x.comm_init_rank || !x.comm_destroy || !x.all_reduce || !x.error_string)
+      snprintf(x.why, sizeof x.why, "RCCL lacks an entry point");
+    return x;
+  }();
+  return r;
+}
+
+int comm_fail(const char* what, ncclResult_t r) {
+  char buf[320];
+  snprintf(buf, sizeof buf, "%s: %s", what, rccl().error_string ? rccl().error_string(r) : "?");
+  return pow_set_error(POW_ECOMM, buf);
+}
+
+int hip_fail(const char* what, hipError_t e) {
+  char buf[320];
+  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  return pow_set_error(POW_EHIP, buf);
+}
+
+constexpr size_t kMaxWords = 8;
+
+}  // namespace
+
+struct pow_group {
+  pow_ctx* ctx = nullptr;
+  int nranks = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+  uint64_t* d_buf = nullptr;  // kMaxWords device words: the all-reduce operand
+  uint64_t* h_buf = nullptr;  // pinned host mirror
+};
+
+namespace {
+
+// In-place all-reduce of n <= kMaxWords u64 on the ctx's stream.
+int group_allreduce(pow_group* g, uint64_t* v, size_t n, ncclRedOp_t op) {
+  hipError_t e = hipSetDevice(pow_ctx_device(g->ctx));
+  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+  hipStream_t st = (hipStream_t)pow_ctx_stream(g->ctx);
+  memcpy(g->h_buf, v, n * sizeof(uint64_t));
+  if ((e = hipMemcpyAsync(g->d_buf, g->h_buf, n * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
+    return hip_fail("hipMemcpyAsync", e);
+  ncclResult_t r = rccl().all_reduce(g->d_buf, g->d_buf, n, ncclUint64, op, g->comm, st);
+  if (r != ncclSuccess) return comm_fail("ncclAllReduce", r);
+  if ((e = hipMemcpyAsync(g->h_buf, g->d_buf, n * 8, hipMemcpyDeviceToHost, st)) != hipSuccess)
+    return hip_fail("hipMemcpyAsync", e);
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+  memcpy(v, g->h_buf, n * sizeof(uint64_t));
+  return POW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void pow_group_partition(uint64_t start, uint64_t count, int rank, int nranks, uint64_t* shard_start,
+                         uint64_t* shard_count) {
+  if (nranks < 1) nranks = 1;
+  const uint64_t base = count / (uint64_t)nranks, extra = count % (uint64_t)nranks;
+  const uint64_t r = (uint64_t)std::max(0, std::min(rank, nranks - 1));
+  if (shard_start) *shard_start = start + r * base + std::min(r, extra);
+  if (shard_count) *shard_count = base + (r < extra ? 1 : 0);
+}
+
+int pow_group_unique_id(uint8_t id[POW_GROUP_ID_BYTES]) {
+  if (!id) return pow_set_error(POW_EINVAL, "null id");
+  const Rccl& R = rccl();
+  if (R.why[0]) return pow_set_error(POW_ECOMM, R.why);
+  ncclUniqueId u;
+  static_assert(sizeof(u) == POW_GROUP_ID_BYTES, "ncclUniqueId size");
+  ncclResult_t r = R.get_unique_id(&u);
+  if (r != ncclSuccess) return comm_fail("ncclGetUniqueId", r);
+  memcpy(id, &u, sizeof u);
+  return POW_OK;
+}
+
+int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
+                   pow_group** out) {
+  if (!out) return pow_set_error(POW_EINVAL, "null out");
+  *out = nullptr;
+  if (!ctx || !id) return pow_set_error(POW_EINVAL, "null ctx/id");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return pow_set_error(POW_EINVAL, "bad rank/nranks");
+  const Rccl& R = rccl();
+  if (R.why[0]) return pow_set_error(POW_ECOMM, R.why);
+  hipError_t e = hipSetDevice(pow_ctx_device(ctx));
+  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+  pow_group* g = new pow_group;
+  g->ctx = ctx;
+  g->nranks = nranks;
+  g->rank = rank;
+  if ((e = hipMalloc(&g->d_buf, kMaxWords * 8)) != hipSuccess ||
+      (e = hipHostMalloc(&g->h_buf, kMaxWords * 8, hipHostMallocDefault)) != hipSuccess) {
+    pow_group_destroy(g);
+    return hip_fail("group buffers", e);
+  }
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  ncclResult_t r = R.comm_init_rank(&g->comm, nranks, u, rank);  // returns once every rank joined
+  if (r != ncclSuccess) {
+    g->comm = nullptr;
+    pow_group_destroy(g);
+    return comm_fail("ncclCommInitRank", r);
+  }
+  *out = g;
+  return POW_OK;
+}
+
+void pow_group_destroy(pow_group* g) {
+  if (!g) return;
+  (void)hipSetDevice(pow_ctx_device(g->ctx));
+  if (g->comm) (void)rccl().comm_destroy(g->comm);
+  (void)hipFree(g->d_buf);
+  if (g->h_buf) (void)hipHostFree(g->h_buf);
+  delete g;
+}
+
+int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op) {
+  if (!g || (n && !vals)) return pow_set_error(POW_EINVAL, "null");
+  if (n > kMaxWords) return pow_set_error(POW_EINVAL, "at most 8 words per all-reduce");
+  ncclRedOp_t o;
+  if (op == POW_REDUCE_MIN) o = ncclMin;
+  else if (op == POW_REDUCE_MAX) o = ncclMax;
+  else if (op == POW_REDUCE_SUM) o = ncclSum;
+  else return pow_set_error(POW_EINVAL, "unknown reduction");
+  if (n == 0) return POW_OK;
+  return group_allreduce(g, vals, n, o);
+}
+
+int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                   uint64_t round_size, unsigned diff_bits, const volatile uint32_t* cancel_word,
+                   uint32_t epoch, pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
+  if (!g || !tmpl || !out) return pow_set_error(POW_EINVAL, "null");
+  if (ctr_start >= POW_COUNTER_LIMIT || ctr_count > POW_COUNTER_LIMIT - ctr_start)
+    return pow_set_error(POW_EINVAL, "counter range past 62^9");
+  if (diff_bits > 256) return pow_set_error(POW_EINVAL, "difficulty > 256 bits");
+  // Default round: 2^30 counters per GPU (~0.13 s at 8 G/s), so the one
+  // all-reduce per round (tens of microseconds) costs well under 1%.
+  if (round_size == 0) round_size = (uint64_t)g->nranks << 30;
+  uint64_t hashes = 0;
+  if (hashes_done) *hashes_done = 0;
+  for (uint64_t done = 0; done < ctr_count;) {
+    const uint64_t n = std::min(round_size, ctr_count - done);
+    uint64_t s = 0, k = 0;
+    pow_group_partition(ctr_start + done, n, g->rank, g->nranks, &s, &k);
+    // {lowest solving counter of this rank's shard, go (0 = cancelled), ok (0 = failed)}
+    uint64_t v[3] = {UINT64_MAX, 1, 1};
+    int local_rc = POW_OK;
+    char local_err[512] = {0};
+    if (k) {
+      pow_block tmp;
+      uint64_t c = 0, h = 0;
+      local_rc = pow_mine(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, &h);
+      hashes += h;
+      if (local_rc == 1) v[0] = c;
+      if (local_rc < 0) {
+        v[2] = 0;
+        snprintf(local_err, sizeof local_err, "%s", pow_last_error());
+      }
+    }
+    if (cancel_word && *cancel_word != epoch) v[1] = 0;
+    if (int rc = group_allreduce(g, v, 3, ncclMin)) return rc;
+    if (hashes_done) *hashes_done = hashes;
+    if (v[2] == 0)  // every rank leaves the search together
+      return local_rc < 0 ? pow_set_error(local_rc, local_err) : pow_set_error(POW_ECOMM, "a peer rank failed");
+    if (v[1] == 0) return 0;  // cancelled on some rank
+    if (v[0] != UINT64_MAX) {
+      *out = *tmpl;
+      if (int rc = pow_nonce_from_counter(v[0], out->nonce)) return rc;
+      char hx[65];
+      if (int rc = pow_hash_block(g->ctx, out, nullptr, hx)) return rc;
+      memcpy(out->block_hash, hx, 65);  // strcpy semantics (node.cpp:318)
+      if (found_ctr) *found_ctr = v[0];
+      return 1;
+    }
+    done += n;
+  }
+  return 0;
+}
+
+}  // extern "C"

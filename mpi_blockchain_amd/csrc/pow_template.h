@@ -89,7 +89,13 @@ struct PowResult {
 #ifdef __cplusplus
 extern "C++" {
 struct pow_block;
+struct pow_ctx;
 // Fill PowConsts from a template block (nonce field ignored).
 void pow_build_consts(const struct pow_block* tmpl, PowConsts* out);
+// Library-internal accessors of a context (used by pow_group.cpp).
+int pow_ctx_device(const struct pow_ctx* ctx);
+void* pow_ctx_stream(const struct pow_ctx* ctx);  // the ctx's hipStream_t
+// Record `msg` for pow_last_error(); returns `code`.
+int pow_set_error(int code, const char* msg);
 }
 #endif

@@ -15,6 +15,7 @@ replacement for "all ranks search, first solution wins".
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Optional
 
 NONE = (1 << 63) - 1  # "no solution" in the int64 all-reduce
@@ -62,6 +63,88 @@ def torch_allreduce_min(device=None, group=None) -> Callable[[int], int]:
         return int(buf.item())
 
     return f
+
+
+class RcclGroup:
+    """The same sharded search done natively: ``pow_group_*`` of
+    libpow_gpu.so (mpi_blockchain_amd/csrc/pow_group.cpp) runs the rounds in
+    C++ and calls RCCL itself (one 24-byte ``ncclAllReduce(ncclMin)`` per
+    round for winner, cancellation and failure).  This is the form a C/C++
+    caller — the reference's node is C++ — uses; ranks exchange the 128-byte
+    RCCL id by any means (``from_torch`` uses torch.distributed)."""
+
+    def __init__(self, miner, rank: int, world: int, unique_id: bytes):
+        from ._lib import GROUP_ID_BYTES, check
+
+        if len(unique_id) != GROUP_ID_BYTES:
+            raise ValueError("unique_id must be 128 bytes")
+        self.miner, self.rank, self.world = miner, rank, world
+        self.g = ctypes.c_void_p()
+        check(miner.L.pow_group_init(miner.ctx, world, rank, unique_id, ctypes.byref(self.g)))
+
+    @staticmethod
+    def make_unique_id() -> bytes:
+        from ._lib import GROUP_ID_BYTES, check, load
+
+        buf = ctypes.create_string_buffer(GROUP_ID_BYTES)
+        check(load().pow_group_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def from_torch(cls, miner, group=None) -> "RcclGroup":
+        """Collective over an initialised torch.distributed process group:
+        rank 0 makes the id, every rank receives it, all join."""
+        import torch.distributed as dist
+
+        obj = [cls.make_unique_id() if dist.get_rank(group) == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls(miner, dist.get_rank(group), dist.get_world_size(group), obj[0])
+
+    def allreduce(self, vals, op: str = "min") -> list[int]:
+        from ._lib import POW_REDUCE_MAX, POW_REDUCE_MIN, POW_REDUCE_SUM, check
+
+        arr = (ctypes.c_uint64 * len(vals))(*vals)
+        code = {"min": POW_REDUCE_MIN, "max": POW_REDUCE_MAX, "sum": POW_REDUCE_SUM}[op]
+        check(self.miner.L.pow_group_allreduce_u64(self.g, arr, len(vals), code))
+        return list(arr)
+
+    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
+             epoch: int | None = None):
+        """Lowest solving counter of [start, start+count) over all ranks (the
+        same MineResult on every rank; ``hashes`` = this rank's trials)."""
+        from ._lib import Block, check
+        from .miner import MineResult
+
+        out = Block()
+        ctr, hashes = ctypes.c_uint64(), ctypes.c_uint64()
+        m = self.miner
+        ep = m.epoch if epoch is None else epoch
+        rc = check(m.L.pow_group_mine(self.g, ctypes.byref(tmpl), start, count, round_size, difficulty,
+                                      ctypes.byref(m._cancel), ep, ctypes.byref(out), ctypes.byref(ctr),
+                                      ctypes.byref(hashes)))
+        if rc == 0:
+            return None
+        return MineResult(out, ctr.value, hashes.value, m.stats()["kernel_ms"])
+
+    def close(self) -> None:
+        if self.g:
+            self.miner.L.pow_group_destroy(self.g)
+            self.g = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def native_partition(start: int, count: int, rank: int, world: int) -> tuple[int, int]:
+    """pow_group_partition of the C ABI (must equal :func:`partition`)."""
+    from ._lib import load
+
+    s, n = ctypes.c_uint64(), ctypes.c_uint64()
+    load().pow_group_partition(start, count, rank, world, ctypes.byref(s), ctypes.byref(n))
+    return s.value, n.value
 
 
 class ShardedMiner:

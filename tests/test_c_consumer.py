@@ -30,3 +30,36 @@ def test_c_consumer_mines_valid_chain(exe):
     p = subprocess.run([exe, "10", "12"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     assert "chain of 10 blocks at difficulty 12: valid" in p.stdout
+
+
+@pytest.fixture(scope="module")
+def mpi_exe(tmp_path_factory):
+    from mpi_blockchain_amd.build import MPI_HOME, build, mpi_available
+
+    if not mpi_available():
+        pytest.skip("no MPI in this image")
+    build()
+    out = str(tmp_path_factory.mktemp("cm") / "group_mine_mpi")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(MPI_HOME, "include"), os.path.join(ROOT, "examples", "group_mine_mpi.c"),
+                    "-L", PKG, "-lpow_gpu", f"-Wl,-rpath,{PKG}", os.path.join(MPI_HOME, "lib", "libmpi.so"),
+                    # the system libstdc++ first: MPICH's lib dir holds an older one
+                    "-Wl,-rpath-link,/lib/x86_64-linux-gnu", f"-Wl,-rpath-link,{os.path.join(MPI_HOME, 'lib')}", "-o", out], check=True)
+    return out
+
+
+def test_group_example_builds(mpi_exe):
+    assert os.path.exists(mpi_exe)
+
+
+@pytest.mark.gpu
+def test_group_example_mines(mpi_exe, tmp_path):
+    """C + MPI caller of the sharded search: the RCCL id over MPI_Bcast, then
+    pow_group_mine; S0 at d = 21 over [0, 2^32): lowest counter 2392323
+    (tests/golden/fingerprints_2p32.json)."""
+    from mpi_blockchain_amd.node import MPIEXEC, mpi_env
+
+    p = subprocess.run(["timeout", "-k", "10", "240", MPIEXEC, "-np", "1", mpi_exe, "21", "32"],
+                       capture_output=True, text=True, cwd=tmp_path, env=mpi_env())
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "counter 2392323 " in p.stdout and "agreed and valid" in p.stdout, p.stdout

@@ -106,3 +106,33 @@ def test_gloo_world2():
     want = [O.mine(b, 0, 1 << 12, 9), O.mine(b, 300, 5000, 9), O.mine(b, 0, 40000, 13)]
     assert want[0] == 263  # golden: first S1 solution
     assert out[0] == out[1] == want
+
+
+def test_native_partition_matches():
+    """pow_group_partition (C ABI, used by pow_group_mine) == shard.partition."""
+    from mpi_blockchain_amd.shard import native_partition
+
+    for count in (0, 1, 7, 62, 1000, 2**32 + 3, 2**40 + 17):
+        for world in (1, 2, 3, 4, 8):
+            for r in range(world):
+                assert native_partition(100, count, r, world) == partition(100, count, r, world)
+
+
+def test_group_unique_id_and_arg_checks():
+    """RCCL loads on demand (no GPU needed for the id); bad arguments are
+    rejected before any RCCL or HIP call."""
+    import ctypes
+
+    from mpi_blockchain_amd import _lib
+    from mpi_blockchain_amd.shard import RcclGroup
+
+    a, b = RcclGroup.make_unique_id(), RcclGroup.make_unique_id()
+    assert len(a) == len(b) == _lib.GROUP_ID_BYTES and a != b
+    L = _lib.load()
+    g = ctypes.c_void_p()
+    assert L.pow_group_init(None, 1, 0, a, ctypes.byref(g)) == _lib.POW_EINVAL and not g
+    assert L.pow_group_unique_id(None) == _lib.POW_EINVAL
+    blk = _lib.Block()
+    assert L.pow_group_mine(None, ctypes.byref(blk), 0, 1, 0, 9, None, 0, ctypes.byref(blk), None, None) \
+        == _lib.POW_EINVAL
+    assert L.pow_group_allreduce_u64(None, None, 0, 0) == _lib.POW_EINVAL

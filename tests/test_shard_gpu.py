@@ -43,3 +43,50 @@ def test_sharded_equals_unsharded():
             assert best == m.mine(b, 0, 1 << 20, 13).counter
     finally:
         dist.destroy_process_group()
+
+
+def test_native_group_world1():
+    """pow_group_mine (C++ rounds + RCCL all-reduce) on one rank returns
+    exactly pow_mine's lowest counter, for one round and for many small
+    rounds; the all-reduce itself; cancellation."""
+    from mpi_blockchain_amd.miner import GpuMiner
+    from mpi_blockchain_amd.shard import RcclGroup
+
+    with GpuMiner(0) as m:
+        with RcclGroup(m, 0, 1, RcclGroup.make_unique_id()) as g:
+            assert g.allreduce([5, 7, 1 << 63], "min") == [5, 7, 1 << 63]
+            assert g.allreduce([3, 4], "sum") == [3, 4]
+            b = make_block(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
+            for d, rs in ((9, 0), (13, 1 << 12), (17, 1 << 20), (13, 5000)):
+                want = m.mine(b, 300, 1 << 24, d)
+                got = g.mine(b, 300, 1 << 24, d, round_size=rs)
+                assert want is not None and got is not None
+                assert got.counter == want.counter
+                assert bytes(got.block.nonce) == bytes(want.block.nonce)
+                assert bytes(got.block.block_hash) == bytes(want.block.block_hash)
+            assert g.mine(b, 0, 263, 9) is None  # golden: the first S1 solution is 263
+            assert g.mine(b, 0, 264, 9, round_size=100).counter == 263
+            m.cancel()
+            assert g.mine(b, 0, 1 << 40, 60, epoch=(m.epoch - 1) & 0xFFFFFFFF) is None
+
+
+def test_native_group_from_torch():
+    """RcclGroup.from_torch: the RCCL id travels over torch.distributed."""
+    import torch.distributed as dist
+
+    from mpi_blockchain_amd.miner import GpuMiner
+    from mpi_blockchain_amd.shard import RcclGroup
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with GpuMiner(0) as m, RcclGroup.from_torch(m) as g:
+            b = make_block(1, 0, 9, 1700000000, b"")
+            r = g.mine(b, 0, 1 << 20, 9)
+            assert r is not None and r.counter == 238  # golden: first S0 solution
+    finally:
+        dist.destroy_process_group()

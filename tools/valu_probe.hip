@@ -41,6 +41,29 @@ __device__ __forceinline__ void op(uint32_t& x, uint32_t y, uint32_t z) {
   if constexpr (OP == 20) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(y));
   if constexpr (OP == 21) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
   if constexpr (OP == 22) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+  if constexpr (OP == 23) asm volatile("v_lshlrev_b32_e32 %0, 3, %0" : "+v"(x));
+  if constexpr (OP == 24) asm volatile("v_or_b32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 25) asm volatile("v_and_b32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 26) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 27) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 28) asm volatile("v_pk_lshrrev_b16 %0, 3, %0" : "+v"(x));
+  if constexpr (OP == 29) asm volatile("v_max_u32_e32 %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 30) asm volatile("v_not_b32_e32 %0, %0" : "+v"(x));
+  if constexpr (OP == 31) asm volatile("v_lshrrev_b32_e64 %0, %1, %0" : "+v"(x) : "v"(y));
+  if constexpr (OP == 32) asm volatile("v_lshlrev_b32_sdwa %0, 3, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "+v"(x));
+  if constexpr (OP == 33) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:DWORD" : "+v"(x) : "v"(y));
+  if constexpr (OP == 34) asm volatile("v_mov_b32_dpp %0, %0 row_ror:3 row_mask:0xf bank_mask:0xf" : "+v"(x));
+  if constexpr (OP == 35) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(x) : "s"(y), "v"(z));
+  if constexpr (OP == 36) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(x) : "s"(y));
+  if constexpr (OP == 37) asm volatile("v_xor_b32_e32 %0, %1, %0" : "+v"(x) : "s"(y));
+  if constexpr (OP == 38) asm volatile("v_add_u32_e32 %0, 0x12345, %0" : "+v"(x));
+  if constexpr (OP == 39) asm volatile("v_lshrrev_b32_e64 %0, %1, %0" : "+v"(x) : "s"(y));
+  if constexpr (OP == 40) asm volatile("v_alignbit_b32 %0, %0, %0, %1" : "+v"(x) : "v"(y));
+  if constexpr (OP == 41) asm volatile("v_add_u32_e64 %0, %0, 7" : "+v"(x));
+  if constexpr (OP == 42) asm volatile("v_bitop3_b32 %0, %0, 7, %1 bitop3:0xca" : "+v"(x) : "v"(z));
+  if constexpr (OP == 43) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(x) : "s"(y));
+  if constexpr (OP == 44) asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(x) : "s"(y));
+  if constexpr (OP == 45) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(x) : "v"(y), "v"(z));
 }
 
 // Mixed streams: one "step" over the 8 chains; instruction order interleaves chains
@@ -92,17 +115,50 @@ __device__ __forceinline__ void pattern(uint32_t& x0, uint32_t& x1, uint32_t& x2
     ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD) ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD)
     ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD) ALL8(A3) ALL8(B3) ALL8(A3) ALL8(AD)
   }
+  if constexpr (P == 10) {  // waves specialise by workgroup parity: odd WGs alignbit only, even WGs bitop3 only
+    if (__builtin_amdgcn_readfirstlane(blockIdx.x) & 1u) {
+      ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB)
+      ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB) ALL8(AB)
+    } else {
+      ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3)
+      ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3) ALL8(B3)
+    }
+  }
+  if constexpr (P == 11) {  // waves specialise: odd WGs add3 only, even WGs add only
+    if (__builtin_amdgcn_readfirstlane(blockIdx.x) & 1u) {
+      ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3)
+      ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3) ALL8(A3)
+    } else {
+      ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD)
+      ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD) ALL8(AD)
+    }
+  }
+  if constexpr (P == 12) {  // shifts + bitop3 only (F2 without xor/add): SR SL B3 x4 = 12 groups... (x8 = 192)
+    ALL8(SR) ALL8(SL) ALL8(B3) ALL8(SR) ALL8(SL) ALL8(B3) ALL8(SR) ALL8(SL) ALL8(B3) ALL8(SR) ALL8(SL) ALL8(B3)
+    ALL8(SR) ALL8(SL) ALL8(B3) ALL8(SR) ALL8(SL) ALL8(B3) ALL8(SR) ALL8(SL) ALL8(B3) ALL8(SR) ALL8(SL) ALL8(B3)
+  }
+  if constexpr (P == 13) {  // shift : add 1:1 (full-rate VOP2 only)
+    ALL8(SR) ALL8(AD) ALL8(SL) ALL8(AD) ALL8(SR) ALL8(AD) ALL8(SL) ALL8(AD)
+    ALL8(SR) ALL8(AD) ALL8(SL) ALL8(AD) ALL8(SR) ALL8(AD) ALL8(SL) ALL8(AD)
+  }
+  if constexpr (P == 14) {  // shift only, alternating right/left (x8 = 128)
+    ALL8(SR) ALL8(SL) ALL8(SR) ALL8(SL) ALL8(SR) ALL8(SL) ALL8(SR) ALL8(SL)
+    ALL8(SR) ALL8(SL) ALL8(SR) ALL8(SL) ALL8(SR) ALL8(SL) ALL8(SR) ALL8(SL)
+  }
   if constexpr (P == 3) {  // bitop3 : add_u32 = 1 : 1 (all full rate)
     ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD)
     ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD) ALL8(B3) ALL8(AD)
   }
 }
-static const int kPatLen[] = {112, 128, 128, 128, 128, 208, 192, 192, 128, 128};
+static const int kPatLen[] = {112, 128, 128, 128, 128, 208, 192, 192, 128, 128, 128, 128, 192, 128, 128};
 static const char* kPatNames[] = {"F0 round as built (6ab:4b3:2a3:2add)", "alignbit:bitop3 1:1",
                                   "alignbit:add 1:1", "bitop3:add 1:1",
                                   "F1 round, adds split (6ab:4b3:6add)", "F2 round, full-rate only (26 ops)",
                                   "alignbit:bitop3:add 1:1:1", "alignbit runs of 24 / full 24",
-                                  "alignbit:full 1:3", "add3:full 1:1"};
+                                  "alignbit:full 1:3", "add3:full 1:1",
+                                  "split waves: alignbit-only WGs + bitop3-only WGs",
+                                  "split waves: add3-only WGs + add-only WGs", "shift:shift:bitop3",
+                                  "shift:add 1:1", "shift only (right/left)"};
 
 template <int P>
 __global__ __launch_bounds__(256) void probe_mix(uint32_t seed, int iters, uint32_t* out,
@@ -220,7 +276,14 @@ static const char* kNames[] = {"v_add_u32_e32", "v_add3_u32", "v_alignbit_b32", 
                                "v_xad_u32", "v_lshrrev_b32_e32", "v_add_u32_e64",
                                "v_alignbit_b32(x,x)", "v_add3_u32(sgpr)", "v_and_or_b32", "v_bfi_b32",
                                "v_perm_b32", "v_alignbyte_b32", "v_bfe_u32", "v_lshl_add_u32", "v_or3_b32",
-                               "v_cndmask_b32_e32", "v_sub_u32_e32", "v_mad_u32_u24"};
+                               "v_cndmask_b32_e32", "v_sub_u32_e32", "v_mad_u32_u24", "v_lshlrev_b32_e32",
+                               "v_or_b32_e32", "v_and_b32_e32", "v_mul_u32_u24_e32", "v_pk_add_u16",
+                               "v_pk_lshrrev_b16", "v_max_u32_e32", "v_not_b32_e32", "v_lshrrev_b32_e64(vgpr amt)",
+                               "v_lshlrev_b32_sdwa", "v_xor_b32_sdwa(WORD_1 preserve)", "v_mov_b32_dpp row_ror",
+                               "v_bitop3_b32(sgpr)", "v_add_u32_e32(sgpr)", "v_xor_b32_e32(sgpr)",
+                               "v_add_u32_e32(literal)", "v_lshrrev_b32_e64(sgpr amt)", "v_alignbit_b32(vgpr amt)",
+                               "v_add_u32_e64(inline const)", "v_bitop3_b32(inline const)", "v_mov_b32(sgpr)",
+                               "v_sub_u32_e32(sgpr)", "v_bitop3_b32 maj"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void probe(uint32_t seed, int iters, uint32_t* out,
@@ -299,6 +362,46 @@ int main() {
   run64<3>(cus, 8, out, d_clk, h_clk);
   run64<4>(cus, 8, out, d_clk, h_clk);
   if (getenv("PROBE_64_ONLY")) return 0;
+  if (getenv("PROBE_R3")) {  // which operand kinds keep an op at the full rate
+    for (int w : {8, 4}) {
+      run<36>(cus, w, out, d_clk, h_clk);
+      run<37>(cus, w, out, d_clk, h_clk);
+      run<38>(cus, w, out, d_clk, h_clk);
+      run<39>(cus, w, out, d_clk, h_clk);
+      run<40>(cus, w, out, d_clk, h_clk);
+      run<41>(cus, w, out, d_clk, h_clk);
+      run<42>(cus, w, out, d_clk, h_clk);
+      run<43>(cus, w, out, d_clk, h_clk);
+      run<44>(cus, w, out, d_clk, h_clk);
+      run<45>(cus, w, out, d_clk, h_clk);
+      run<0>(cus, w, out, d_clk, h_clk);
+      run<3>(cus, w, out, d_clk, h_clk);
+    }
+    return 0;
+  }
+  if (getenv("PROBE_R2")) {  // round-1 follow-up: wave specialisation, more full-rate candidates
+    run_mix<10>(cus, 8, out, d_clk, h_clk);
+    run_mix<11>(cus, 8, out, d_clk, h_clk);
+    run_mix<12>(cus, 8, out, d_clk, h_clk);
+    run_mix<13>(cus, 8, out, d_clk, h_clk);
+    run_mix<14>(cus, 8, out, d_clk, h_clk);
+    run_mix<0>(cus, 8, out, d_clk, h_clk);
+    run_mix<1>(cus, 8, out, d_clk, h_clk);
+    run<23>(cus, 8, out, d_clk, h_clk);
+    run<24>(cus, 8, out, d_clk, h_clk);
+    run<25>(cus, 8, out, d_clk, h_clk);
+    run<26>(cus, 8, out, d_clk, h_clk);
+    run<27>(cus, 8, out, d_clk, h_clk);
+    run<28>(cus, 8, out, d_clk, h_clk);
+    run<29>(cus, 8, out, d_clk, h_clk);
+    run<30>(cus, 8, out, d_clk, h_clk);
+    run<31>(cus, 8, out, d_clk, h_clk);
+    run<32>(cus, 8, out, d_clk, h_clk);
+    run<33>(cus, 8, out, d_clk, h_clk);
+    run<34>(cus, 8, out, d_clk, h_clk);
+    run<35>(cus, 8, out, d_clk, h_clk);
+    return 0;
+  }
   for (int w : {8}) {
     run_mix<0>(cus, w, out, d_clk, h_clk);
     run_mix<4>(cus, w, out, d_clk, h_clk);
