@@ -165,6 +165,8 @@ struct pow_ctx {
   PowConsts* d_consts = nullptr;
   PowResult* d_res = nullptr;
   PowResult* h_res = nullptr;  // pinned
+  uint32_t* d_tail = nullptr;  // sweep: per-wave remainders (< 32 each), appended after the launch
+  uint32_t tail_cap = 0;
   uint32_t* d_out = nullptr;   // pow_sweep's device list and its radix-sort twin
   uint32_t* d_alt = nullptr;
   void* d_sort_tmp = nullptr;
@@ -231,6 +233,8 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   if (rc) return rc;
   PowResult init{};
   init.min_rel = ~0ull;
+  init.tail_buf = ctx->d_tail;
+  init.tail_cap = ctx->tail_cap;
   HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
   const unsigned grid = grid_for(ctx, L.n_prefix);
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
@@ -338,6 +342,8 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipMalloc(&ctx->d_consts, sizeof(PowConsts)), "hipMalloc consts");
   chk(hipMalloc(&ctx->d_res, sizeof(PowResult)), "hipMalloc result");
   chk(hipHostMalloc(&ctx->h_res, sizeof(PowResult), hipHostMallocDefault), "hipHostMalloc");
+  ctx->tail_cap = ctx->grid_full * 4u * 32u;  // < 32 per wave, 4 waves per workgroup
+  chk(hipMalloc(&ctx->d_tail, (size_t)ctx->tail_cap * sizeof(uint32_t)), "hipMalloc sweep tail");
   if (rc != POW_OK) {
     pow_destroy(ctx);
     return rc;
@@ -352,6 +358,7 @@ void pow_destroy(pow_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   (void)hipFree(ctx->d_consts);
   (void)hipFree(ctx->d_res);
+  (void)hipFree(ctx->d_tail);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_alt);
   (void)hipFree(ctx->d_sort_tmp);
@@ -511,7 +518,17 @@ int pow_sweep_device(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   if (int rc = upload_consts(ctx, tmpl)) return rc;
   const uint32_t cap32 = (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu);
   if (int rc = run_search(ctx, ctr_start, ctr_count, diff_bits, 0, dev_out, cap32)) return rc;
-  if (n_found) *n_found = ctx->h_res->count;
+  // The kernel writes 32-entry blocks to dev_out and each wave's last < 32
+  // solutions to ctx->d_tail: append those behind the blocks.
+  const uint64_t nblk = ctx->h_res->count, ntail = ctx->h_res->tail;
+  if (ntail > ctx->tail_cap) return fail(POW_EHIP, "sweep tail overflow (%llu)", (unsigned long long)ntail);
+  if (ntail && nblk < cap32) {
+    const uint64_t k = std::min<uint64_t>(ntail, cap32 - nblk);
+    HIP_OK(hipMemcpyAsync(dev_out + nblk, ctx->d_tail, k * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+  }
+  if (n_found) *n_found = nblk + ntail;
   if (min_ctr && ctx->h_res->min_rel != ~0ull) *min_ctr = ctr_start + ctx->h_res->min_rel;
   return POW_OK;
 }

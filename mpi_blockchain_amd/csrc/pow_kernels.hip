@@ -72,15 +72,46 @@ __device__ __forceinline__ void const_chunk(St& t, cptr kwbase, uint32_t dep) {
   }
 }
 
-// Append a wave's staged solutions (n <= 128, in LDS) to the global list with
-// one atomic: lanes store consecutive entries (coalesced).
-__device__ __forceinline__ void flush_stage(const uint32_t* wst, uint32_t n, uint32_t lane,
-                                            PowResult* res, uint32_t* out, uint32_t cap) {
+// Append the 32-entry-aligned part of a wave's staged solutions (nst <= 127,
+// in LDS) to the global list with one atomic; the remainder (< 32) moves to
+// the stage front.  Every reservation is a multiple of 32 entries, so each
+// block starts on a 128-byte line of `out` (hipMalloc alignment) and lanes
+// write it as whole lines, 16 B per lane: no line is written in parts by two
+// waves (with 4-B lanes at arbitrary offsets the memory-side write requests
+// were 2.3x the list's bytes, profiles/r01/final/pmc_summary.json).
+__device__ __forceinline__ void flush_stage(uint32_t* wst, uint32_t& nst, uint32_t lane, PowResult* res,
+                                            uint32_t* out, uint32_t cap) {
+  const uint32_t n = nst & ~31u;
   uint32_t got = 0;
   if (lane == 0) got = atomicAdd(&res->count, n);
   const uint32_t base = __builtin_amdgcn_readfirstlane(got);
-  for (uint32_t i = lane; i < n; i += 64u)
-    if (base + i < cap) out[base + i] = wst[i];
+  const uint32_t i = lane * 4u;  // n <= 96: one pass of <= 24 lanes
+  if (i < n) {
+    const uint32_t e0 = wst[i], e1 = wst[i + 1u], e2 = wst[i + 2u], e3 = wst[i + 3u];
+    if (base + i + 4u <= cap && ((uintptr_t)out & 15u) == 0) {
+      *reinterpret_cast<uint4*>(out + base + i) = make_uint4(e0, e1, e2, e3);
+    } else {
+      if (base + i < cap) out[base + i] = e0;
+      if (base + i + 1u < cap) out[base + i + 1u] = e1;
+      if (base + i + 2u < cap) out[base + i + 2u] = e2;
+      if (base + i + 3u < cap) out[base + i + 3u] = e3;
+    }
+  }
+  const uint32_t rem = nst - n;  // source [n, n + rem) and target [0, rem) do not overlap (n >= 32 > rem)
+  const uint32_t t = lane < rem ? wst[n + lane] : 0u;
+  if (lane < rem) wst[lane] = t;
+  nst = rem;
+}
+
+// A wave's last staged solutions (< 32) go to the side list res->tail_buf; the
+// host appends it to the main list after the launch.
+__device__ __forceinline__ void flush_tail(const uint32_t* wst, uint32_t nst, uint32_t lane, PowResult* res) {
+  uint32_t got = 0;
+  if (lane == 0) got = atomicAdd(&res->tail, nst);
+  const uint32_t base = __builtin_amdgcn_readfirstlane(got);
+  uint32_t* const tail = res->tail_buf;
+  const uint32_t tail_cap = res->tail_cap;
+  if (lane < nst && base + lane < tail_cap) tail[base + lane] = wst[lane];
 }
 
 // Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
@@ -105,17 +136,17 @@ __device__ __forceinline__ bool full_test(const uint32_t H[8], uint32_t d) {
 // (MI355X_MICROARCH.md "Residency") gives 8 per CU only at <= 80; at the
 // compiler's natural ~92 it is 7.
 template <int MODE, bool FULL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8))) void pow_search(
     const PowConsts* __restrict__ C, PowLaunch L, uint32_t* __restrict__ out,
     PowResult* __restrict__ res) {
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t iters = 0;
-  // Sweep mode: solutions are staged per wave in LDS and flushed in batches
-  // (one atomic + coalesced stores per >= 64 solutions); the lowest solution
+  // Sweep mode: solutions are staged per wave in LDS and flushed in 32-entry
+  // blocks (one atomic + whole-line stores per >= 64 solutions); the lowest solution
   // is kept per lane and min-reduced once per wave at exit.  One atomic per
   // solution would make every solution a separate memory-side request
   // (~0.68 GB of requests per 2^32 sweep at d = 9 for 34 MB of data).
-  __shared__ uint32_t stage[4][128];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[4][128];
   uint32_t* wst = stage[threadIdx.x >> 6];
   uint32_t nst = 0;                     // staged entries (wave-uniform)
   unsigned long long mymin = ~0ull;     // lowest solution of this lane
@@ -278,17 +309,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
           if (ok) wst[nst + rank] = relv;
           nst += (uint32_t)__popcll(m);
-          if (nst >= 64) {
-            flush_stage(wst, nst, lane, res, out, L.cap);
-            nst = 0;
-          }
+          if (nst >= 64) flush_stage(wst, nst, lane, res, out, L.cap);
         }
       }
     }
     if (MODE == 2 && stop) break;
   }
   if (MODE == 0) {
-    if (nst) flush_stage(wst, nst, lane, res, out, L.cap);
+    if (nst >= 32) flush_stage(wst, nst, lane, res, out, L.cap);
+    if (nst) flush_tail(wst, nst, lane, res);
     // wave min of the per-lane minima, one atomic per wave
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

@@ -81,9 +81,12 @@ struct PowLaunch {
 struct PowResult {
   unsigned long long min_rel;  // lowest solving (counter - ctr_start); ~0 = none
   unsigned long long hashes;   // mine mode: trials actually computed
-  unsigned int count;          // number of solutions (sweep)
+  unsigned int count;          // sweep: solutions in the main list (32-entry blocks)
   unsigned int next;           // next prefix chunk to hand out (dynamic work queue)
-  unsigned int pad[2];
+  unsigned int tail;           // sweep: solutions in tail_buf (< 32 per wave)
+  unsigned int tail_cap;       // entries of tail_buf
+  unsigned int* tail_buf;      // sweep: each wave's last < 32 solutions (appended by the host);
+                               // read from here at wave exit, not held in SGPRs all kernel long
 };
 
 #ifdef __cplusplus
