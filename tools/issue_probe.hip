@@ -145,6 +145,14 @@ void sweep(int cus, uint32_t* out, unsigned long long* d_clk, unsigned long long
   run<P, BAR>(cus, 1024, 2, out, d_clk, h_clk);
 }
 
+template <int P, int BAR>
+void sweep_lockstep(int cus, uint32_t* out, unsigned long long* d_clk, unsigned long long* h_clk) {
+  // waves of one workgroup share each SIMD (2 or 4 per SIMD), optionally re-aligned by s_barrier
+  run<P, BAR>(cus, 512, 1, out, d_clk, h_clk);
+  run<P, BAR>(cus, 1024, 1, out, d_clk, h_clk);
+  run<P, BAR>(cus, 1024, 2, out, d_clk, h_clk);
+}
+
 int main() {
   int dev = 0;
   hipDeviceProp_t prop;
@@ -156,6 +164,18 @@ int main() {
   (void)hipMalloc(&out, 64);
   (void)hipMalloc(&d_clk, 16 * cus * 16);
   h_clk = (unsigned long long*)malloc(16 * cus * 16);
+  if (getenv("PROBE_LOCKSTEP")) {  // barrier cost on pure streams, and mixed streams in step
+    sweep_lockstep<1, 0>(cus, out, d_clk, h_clk);
+    sweep_lockstep<1, 4>(cus, out, d_clk, h_clk);
+    sweep_lockstep<1, 16>(cus, out, d_clk, h_clk);
+    sweep_lockstep<0, 16>(cus, out, d_clk, h_clk);
+    sweep_lockstep<3, 0>(cus, out, d_clk, h_clk);
+    sweep_lockstep<3, 4>(cus, out, d_clk, h_clk);
+    sweep_lockstep<3, 16>(cus, out, d_clk, h_clk);
+    sweep_lockstep<5, 4>(cus, out, d_clk, h_clk);
+    sweep_lockstep<5, 16>(cus, out, d_clk, h_clk);
+    return 0;
+  }
   sweep<0, 0>(cus, out, d_clk, h_clk);
   sweep<1, 0>(cus, out, d_clk, h_clk);
   sweep<2, 0>(cus, out, d_clk, h_clk);
