@@ -162,9 +162,12 @@ struct pow_ctx {
   char name[256] = {0};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  PowConsts* d_consts = nullptr;
-  PowResult* d_res = nullptr;
-  PowResult* h_res = nullptr;  // pinned
+  PowBlob* d_blob = nullptr;   // per-template constants + result words, one allocation
+  PowBlob* h_blob = nullptr;   // pinned staging copy: uploaded with one H2D per launch
+  bool consts_dirty = false;   // h_blob->consts not yet on the device
+  PowConsts* d_consts = nullptr;  // = &d_blob->consts
+  PowResult* d_res = nullptr;     // = &d_blob->res
+  PowResult* h_res = nullptr;  // pinned read-back of d_res
   uint32_t* d_tail = nullptr;  // sweep: per-wave remainders (< 32 each), appended after the launch
   uint32_t tail_cap = 0;
   uint32_t* d_out = nullptr;   // pow_sweep's device list and its radix-sort twin
@@ -182,6 +185,9 @@ struct pow_ctx {
 };
 
 namespace {
+
+int stage_result(pow_ctx* ctx, bool with_tail);
+void digest_out(const uint32_t* h, uint8_t* digest, char* hex);
 
 int set_dev(const pow_ctx* ctx) {
   HIP_OK(hipSetDevice(ctx->device));
@@ -231,11 +237,7 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   PowLaunch L;
   int rc = make_launch(start, count, diff, cap, mode, &L);
   if (rc) return rc;
-  PowResult init{};
-  init.min_rel = ~0ull;
-  init.tail_buf = ctx->d_tail;
-  init.tail_cap = ctx->tail_cap;
-  HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+  if (int rc2 = stage_result(ctx, true)) return rc2;
   const unsigned grid = grid_for(ctx, L.n_prefix);
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_OK(pow_launch_search((int)mode, diff > 32 || ctx->force_full, grid, ctx->stream, ctx->d_consts, L, dev_out,
@@ -264,9 +266,7 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   L.count = count;
   L.diff = diff;
   L.thr = diff >= 32 ? 0u : (0xFFFFFFFFu >> diff);
-  PowResult init{};
-  init.min_rel = ~0ull;
-  HIP_OK(hipMemcpyAsync(ctx->d_res, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+  if (int rc = stage_result(ctx, false)) return rc;
   // A 256-thread workgroup puts one wave on each SIMD of its CU.
   const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
@@ -284,11 +284,48 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   return POW_OK;
 }
 
+// The template's constants go into the pinned staging blob; the next launch
+// uploads them together with its result words (one H2D copy).
 int upload_consts(pow_ctx* ctx, const pow_block* tmpl) {
-  PowConsts C;
-  pow_build_consts(tmpl, &C);
-  HIP_OK(hipMemcpyAsync(ctx->d_consts, &C, sizeof C, hipMemcpyHostToDevice, ctx->stream));
+  pow_build_consts(tmpl, &ctx->h_blob->consts);
+  ctx->consts_dirty = true;
   return POW_OK;
+}
+
+// Reset the device result words (and upload pending constants) before a launch.
+int stage_result(pow_ctx* ctx, bool with_tail) {
+  PowResult& r = ctx->h_blob->res;
+  memset(&r, 0, sizeof r);
+  r.min_rel = ~0ull;
+  if (with_tail) {
+    r.tail_buf = ctx->d_tail;
+    r.tail_cap = ctx->tail_cap;
+  }
+  const size_t off = ctx->consts_dirty ? 0 : offsetof(PowBlob, res);
+  HIP_OK(hipMemcpyAsync((char*)ctx->d_blob + off, (const char*)ctx->h_blob + off, sizeof(PowBlob) - off,
+                        hipMemcpyHostToDevice, ctx->stream));
+  ctx->consts_dirty = false;
+  return POW_OK;
+}
+
+// picosha2's output_hex (picosha2.h:141-150): big-endian digest bytes, lowercase hex.
+void digest_out(const uint32_t* h, uint8_t* digest, char* hex) {
+  static const char hexd[] = "0123456789abcdef";
+  uint8_t d[32];
+  for (int k = 0; k < 8; ++k) {
+    d[4 * k] = (uint8_t)(h[k] >> 24);
+    d[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    d[4 * k + 2] = (uint8_t)(h[k] >> 8);
+    d[4 * k + 3] = (uint8_t)h[k];
+  }
+  if (digest) memcpy(digest, d, 32);
+  if (hex) {
+    for (int k = 0; k < 32; ++k) {
+      hex[2 * k] = hexd[d[k] >> 4];
+      hex[2 * k + 1] = hexd[d[k] & 15];
+    }
+    hex[64] = 0;
+  }
 }
 
 }  // namespace
@@ -339,8 +376,12 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
   chk(hipEventCreate(&ctx->ev0), "hipEventCreate");
   chk(hipEventCreate(&ctx->ev1), "hipEventCreate");
-  chk(hipMalloc(&ctx->d_consts, sizeof(PowConsts)), "hipMalloc consts");
-  chk(hipMalloc(&ctx->d_res, sizeof(PowResult)), "hipMalloc result");
+  chk(hipMalloc(&ctx->d_blob, sizeof(PowBlob)), "hipMalloc consts/result");
+  chk(hipHostMalloc(&ctx->h_blob, sizeof(PowBlob), hipHostMallocDefault), "hipHostMalloc staging");
+  if (ctx->d_blob) {
+    ctx->d_consts = &ctx->d_blob->consts;
+    ctx->d_res = &ctx->d_blob->res;
+  }
   chk(hipHostMalloc(&ctx->h_res, sizeof(PowResult), hipHostMallocDefault), "hipHostMalloc");
   ctx->tail_cap = ctx->grid_full * 4u * 32u;  // < 32 per wave, 4 waves per workgroup
   chk(hipMalloc(&ctx->d_tail, (size_t)ctx->tail_cap * sizeof(uint32_t)), "hipMalloc sweep tail");
@@ -356,8 +397,8 @@ void pow_destroy(pow_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  (void)hipFree(ctx->d_consts);
-  (void)hipFree(ctx->d_res);
+  (void)hipFree(ctx->d_blob);
+  if (ctx->h_blob) (void)hipHostFree(ctx->h_blob);
   (void)hipFree(ctx->d_tail);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_alt);
@@ -476,26 +517,8 @@ int pow_hash_blocks(pow_ctx* ctx, const pow_block* blocks, size_t n, uint8_t* di
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats = pow_stats{ms, 1u, (uint64_t)n};
-  static const char hexd[] = "0123456789abcdef";  // picosha2.h:141-150 (lowercase)
-  for (size_t i = 0; i < n; ++i) {
-    uint8_t d[32];
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t v = dg[i * 8 + k];
-      d[4 * k] = (uint8_t)(v >> 24);
-      d[4 * k + 1] = (uint8_t)(v >> 16);
-      d[4 * k + 2] = (uint8_t)(v >> 8);
-      d[4 * k + 3] = (uint8_t)v;
-    }
-    if (digests) memcpy(digests + 32 * i, d, 32);
-    if (hex) {
-      char* hx = hex + 65 * i;
-      for (int k = 0; k < 32; ++k) {
-        hx[2 * k] = hexd[d[k] >> 4];
-        hx[2 * k + 1] = hexd[d[k] & 15];
-      }
-      hx[64] = 0;
-    }
-  }
+  for (size_t i = 0; i < n; ++i)
+    digest_out(&dg[i * 8], digests ? digests + 32 * i : nullptr, hex ? hex + 65 * i : nullptr);
   return POW_OK;
 }
 
@@ -614,13 +637,23 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
     first = false;
     done += n;
     if (ctx->h_res->min_rel != ~0ull) {
-      const uint64_t ctr = s0 + ctx->h_res->min_rel;
+      const PowResult& r = *ctx->h_res;
+      const uint64_t ctr = s0 + r.min_rel;
       *out = *tmpl;
       pow_nonce_from_counter(ctr, out->nonce);
       char hx[65];
-      const pow_stats keep = ctx->stats;
-      if (int rc = pow_hash_blocks(ctx, out, 1, nullptr, hx)) return rc;
-      ctx->stats = keep;
+      // The latency kernel records its hits with their digests; otherwise (or
+      // if the winner was not among the first POW_HITS) K2 hashes the winner.
+      const PowHit* h = nullptr;
+      for (uint32_t k = 0; lat && k < std::min<uint32_t>(r.nhit, POW_HITS); ++k)
+        if (r.hit[k].rel == r.min_rel) h = &r.hit[k];
+      if (h) {
+        digest_out(h->digest, nullptr, hx);
+      } else {
+        const pow_stats keep = ctx->stats;
+        if (int rc = pow_hash_blocks(ctx, out, 1, nullptr, hx)) return rc;
+        ctx->stats = keep;
+      }
       memcpy(out->block_hash, hx, 65);  // strcpy semantics (node.cpp:318)
       if (found_ctr) *found_ctr = ctr;
       if (hashes_done) *hashes_done = ctx->stats.hashes;

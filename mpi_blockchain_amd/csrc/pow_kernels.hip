@@ -10,11 +10,11 @@
 //
 // Work decomposition of K1 (DESIGN.md "Kernel K1"): counter c = 62*P + j.
 //   * one LANE owns a prefix P (nonce chars 0..7, message words W1, W2);
-//     the prefix-dependent rounds 1-2 and schedule terms are computed once
-//     per prefix, then
+//     the prefix-dependent rounds 1-2 (and all of round 3 but its K+W3 add)
+//     and schedule terms are computed once per prefix, then
 //   * the lane loops over j = 0..61 (the last nonce char, word W3) — j is
 //     wave-uniform, so W3 and every term derived from it are scalar loads.
-//   Per trial the lane runs chunk-0 rounds 3..63 and chunks 1-4 (whose K+W
+//   Per trial the lane runs chunk-0 rounds 4..63 and chunks 1-4 (whose K+W
 //   come from SGPRs: template-constant schedule) — no memory traffic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -198,6 +198,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
     const uint32_t c24 = W17 + C->u24;
     const uint32_t c31 = ssig0(W16) + C->w15;
     const uint32_t c32 = ssig0(W17) + W16;
+    // Round 3 adds K[3] + W3(j) to a per-prefix T1 and nothing else depends
+    // on j: a4 = A3 + kw3(j), e4 = E3 + kw3(j) (2 adds per trial, not 14 ops).
+    const uint32_t P3 = s2.h + bsig1(s2.e) + ch(s2.e, s2.f, s2.g);
+    const uint32_t A3 = P3 + bsig0(s2.a) + maj(s2.a, s2.b, s2.c);
+    const uint32_t E3 = s2.d + P3;
 
     bool stop = false;
     for (uint32_t j = 0; j < POW_J; ++j) {
@@ -218,11 +223,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         }
       }
       ++iters;
-      // ---------------- chunk 0, rounds 3..63 ----------------
+      // ---------------- chunk 0, rounds 4..63 ----------------
       cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
       cptr J = pin(Cb, s2.a ^ j);  // per-j words and the chunk-0 uniform terms
-      St s = s2;
-      round_kw(s, J[PC_KW3 + j]);
+      const uint32_t kw3 = J[PC_KW3 + j];
+      St s{A3 + kw3, s2.a, s2.b, s2.c, E3 + kw3, s2.e, s2.f, s2.g};
 #pragma unroll
       for (int i = 4; i < 16; ++i) round_kw(s, J[PC_KW0 + i]);
       cptr Kp = pin(Cb + PC_K, s.e);  // K[16..63], streamed like the K+W words
@@ -416,15 +421,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     }
     St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
     const_chunk(t, as_const(C->kw[3]), H[0]);
-    const uint32_t h0 = H[0] + t.a;
-    bool hit = h0 <= L.thr;
-    if (FULL && hit) {
-      uint32_t D[8] = {h0, H[1] + t.b, H[2] + t.c, H[3] + t.d,
-                       H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
-      hit = full_test(D, L.diff);
-    }
-    if (__builtin_expect(hit, 0) && (unsigned long long)rel < L.count)
+    // The whole digest stays live here (this kernel runs at <= 4 waves/SIMD,
+    // so the 7 extra VGPRs cost no residency): a hit records it, and the
+    // winner's block_hash needs no K2 launch (one serial SHA-256 of 5 chunks
+    // in one lane is ~15 us, as long as this whole kernel at low d).
+    const uint32_t D[8] = {H[0] + t.a, H[1] + t.b, H[2] + t.c, H[3] + t.d,
+                           H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
+    bool hit = D[0] <= L.thr;
+    if (FULL && hit) hit = full_test(D, L.diff);
+    if (__builtin_expect(hit, 0) && (unsigned long long)rel < L.count) {
       atomicMin(&res->min_rel, (unsigned long long)rel);
+      const uint32_t slot = atomicAdd(&res->nhit, 1u);
+      if (slot < POW_HITS) {
+        res->hit[slot].rel = rel;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) res->hit[slot].digest[k] = D[k];
+      }
+    }
   }
   if (lane == 0) atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);
 }

@@ -77,6 +77,14 @@ struct PowLaunch {
   uint32_t mode;           // 0 = sweep (record all), 1 = mine (lowest + early exit)
 };
 
+// A solution recorded with its digest by the latency kernel, so the winner's
+// block_hash needs no second hashing launch.
+#define POW_HITS 8
+struct PowHit {
+  unsigned long long rel;  // counter - ctr_start
+  uint32_t digest[8];      // H0..H7
+};
+
 // Device-side result words of one launch (zeroed / ~0 before each launch).
 struct PowResult {
   unsigned long long min_rel;  // lowest solving (counter - ctr_start); ~0 = none
@@ -87,6 +95,16 @@ struct PowResult {
   unsigned int tail_cap;       // entries of tail_buf
   unsigned int* tail_buf;      // sweep: each wave's last < 32 solutions (appended by the host);
                                // read from here at wave exit, not held in SGPRs all kernel long
+  unsigned int nhit;           // latency kernel: solutions found (the first POW_HITS are in hit[])
+  unsigned int pad2;
+  PowHit hit[POW_HITS];
+};
+
+// Constants and result words of a context, contiguous so that one H2D copy
+// from a pinned staging twin refreshes both before a launch.
+struct PowBlob {
+  PowConsts consts;
+  alignas(256) PowResult res;
 };
 
 #ifdef __cplusplus

@@ -129,6 +129,8 @@ def test_mine_lowest_counter(mminer, golden, templates):
             assert field(r.block, "nonce") == nonce_from_counter(r.counter)
             hx = block_hex(r.block)
             assert hx == mminer.block_to_hash(r.block)
+            # the winner's digest (recorded by the latency kernel, or K2) vs standard SHA-256
+            assert hx == hashlib.sha256(block_to_str(r.block)).hexdigest()
             assert field(r.block, "block_hash")[64] == 0
             assert field(r.block, "block_hash")[65:] == field(b, "block_hash")[65:]
             assert r.hashes >= r.counter - w["start"]
@@ -164,6 +166,7 @@ def test_mine_any_returns_a_solution(mminer, golden, templates):
                 assert rel in set(s["counters"])
             hx = block_hex(r.block)
             assert hx == mminer.block_to_hash(r.block)
+            assert hx == hashlib.sha256(block_to_str(r.block)).hexdigest()
             assert 256 - int(hx, 16).bit_length() >= int(d)
 
 
