@@ -235,6 +235,27 @@ def test_full_window_2p32(miner, fingerprints, templates):
         assert mn == lad[d]["first"][0]
 
 
+def test_mine_full_window_ladder(mminer, fingerprints, templates):
+    """pow_mine over S0's [0, 2^32) at every rung (K1' for d <= 21, K1 sub-rounds
+    above): the lowest solving counter, then each next one when the search
+    starts just past the previous, equal the CPU fingerprints' first counters;
+    pow_mine_any returns a valid solution of the window.  Winner hashes vs
+    standard SHA-256."""
+    b = block_from_template(templates["S0"])
+    for d, lad in fingerprints["ladder"].items():
+        start = 0
+        for want in lad["first"][:3]:
+            r = mminer.mine(b, start, (1 << 32) - start, int(d))
+            assert r is not None and r.counter == want
+            assert block_hex(r.block) == hashlib.sha256(block_to_str(r.block)).hexdigest()
+            start = want + 1
+        r = mminer.mine(b, 0, 1 << 32, int(d), any_solution=True)
+        assert r is not None and 0 <= r.counter < 1 << 32
+        hx = block_hex(r.block)
+        assert hx == hashlib.sha256(block_to_str(r.block)).hexdigest()
+        assert 256 - int(hx, 16).bit_length() >= int(d)
+
+
 def test_random_templates_vs_oracle(miner):
     """Fresh random templates (arbitrary header fields, binary or hex-string
     prev hashes, random window starts): GPU sweep == C-oracle sweep."""
