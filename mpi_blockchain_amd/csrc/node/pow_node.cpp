@@ -24,12 +24,15 @@
 //     TAG_NEW_BLOCK messages, so two ranks asking each other cannot deadlock
 //     (node.cpp:161 blocks inside the mutex); the miner copies the last block
 //     under the mutex (node.cpp:292 reads it unlocked); a missing ancestor
-//     ends send_blockchain's walk instead of throwing (node.cpp:348).
+//     ends send_blockchain's walk instead of throwing (node.cpp:348); the
+//     receive loop polls with a backoff instead of MPICH's spinning probe
+//     (T12: the reference burns a core per rank there).
 //
 //   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS]
 #include <mpi.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <chrono>
@@ -65,6 +68,23 @@ struct Options {
   unsigned round_log2 = 32; // counters per pow_mine call
   unsigned pause_ms = 0;    // sleep before each round (lets slower CPU ranks compete in tests)
 };
+
+// MPI_Probe that sleeps between polls instead of spinning.  MPICH's blocking
+// probe/receive busy-polls, so every reference rank burns a core in its
+// receive loop on top of its mining thread (node.cpp:404).
+// Here the GPU does the mining, so the receive thread should not take a core:
+// it polls with MPI_Iprobe and backs off from 5 us to 200 us while idle (the
+// first polls after a message stay fast, so a burst is served at full speed).
+void probe_any(MPI_Status* st) {
+  int flag = 0;
+  unsigned nap_us = 5;
+  for (;;) {
+    MPI_Iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, &flag, st);
+    if (flag) return;
+    std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+    nap_us = std::min(200u, nap_us * 2);
+  }
+}
 
 std::string hash_of(const pow_block& b) { return std::string(b.block_hash); }
 std::string prev_of(const pow_block& b) { return std::string(b.previous_block_hash); }
@@ -189,7 +209,7 @@ class Node {
     std::vector<pow_block> chain(kValidationBlocks);
     for (;;) {
       MPI_Status st;
-      MPI_Probe(MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, &st);
+      probe_any(&st);
       if (st.MPI_TAG == kTagChainResponse && st.MPI_SOURCE == owner) {
         MPI_Recv(chain.data(), kValidationBlocks, block_type_, owner, kTagChainResponse, MPI_COMM_WORLD, &st);
         break;
@@ -374,7 +394,10 @@ int Node::run() {
   genesis_.created_at = (uint64_t)time(nullptr);
   last_ = &genesis_;
 
-  std::thread miner([this] { proof_of_work(); });
+  std::thread miner([this] {
+    pthread_setname_np(pthread_self(), "pow_miner");
+    proof_of_work();
+  });
   for (;;) {  // node.cpp:398-420
     pow_block buf;
     MPI_Status st;
@@ -383,7 +406,7 @@ int Node::run() {
       st = deferred_.front().second;
       deferred_.pop_front();
     } else {
-      MPI_Probe(MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, &st);
+      probe_any(&st);
       if (st.MPI_TAG == kTagChainResponse) {  // not waiting for one: drop it
         std::vector<pow_block> junk(kValidationBlocks);
         MPI_Recv(junk.data(), kValidationBlocks, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);

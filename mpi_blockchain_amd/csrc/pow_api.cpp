@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include "../../include/pow_gpu.h"
@@ -162,6 +164,7 @@ struct pow_ctx {
   char name[256] = {0};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_block = nullptr;  // polled with sleeps during long launches
   PowBlob* d_blob = nullptr;   // per-template constants + result words, one allocation
   PowBlob* h_blob = nullptr;   // pinned staging copy: uploaded with one H2D per launch
   bool consts_dirty = false;   // h_blob->consts not yet on the device
@@ -244,6 +247,19 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
                            ctx->d_res));
   HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
+  // Long launches (>= 2^26 counters, >= 8 ms): poll an event every 50 us
+  // instead of spinning a host core for the whole kernel (a
+  // protocol rank should not burn a core while its GPU mines; hipEvent-
+  // Synchronize spins, blocking-sync event or not).  At most 50 us late on a
+  // >= 8 ms launch.  Short launches keep the spin wait: their latency is the
+  // whole time-to-block at low difficulty.
+  if (count >= (1ull << 26)) {
+    HIP_OK(hipEventRecord(ctx->ev_block, ctx->stream));
+    hipError_t q;
+    while ((q = hipEventQuery(ctx->ev_block)) == hipErrorNotReady)
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    HIP_OK(q);
+  }
   HIP_OK(hipStreamSynchronize(ctx->stream));
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -376,6 +392,7 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
   chk(hipEventCreate(&ctx->ev0), "hipEventCreate");
   chk(hipEventCreate(&ctx->ev1), "hipEventCreate");
+  chk(hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming), "hipEventCreate");
   chk(hipMalloc(&ctx->d_blob, sizeof(PowBlob)), "hipMalloc consts/result");
   chk(hipHostMalloc(&ctx->h_blob, sizeof(PowBlob), hipHostMallocDefault), "hipHostMalloc staging");
   if (ctx->d_blob) {
@@ -408,6 +425,7 @@ void pow_destroy(pow_ctx* ctx) {
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->ev_block) (void)hipEventDestroy(ctx->ev_block);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
