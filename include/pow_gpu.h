@@ -21,7 +21,8 @@
  *     gives the text).
  *   - A pow_ctx is bound to one GPU and is NOT thread-safe: exactly one
  *     thread (that rank's mining thread) drives it.  The only cross-thread
- *     input is the cancel word passed to pow_mine, which any thread may bump.
+ *     inputs are the cancel word passed to pow_mine, which any thread may
+ *     bump, and pow_cancel (one other thread).
  *   - The caller owns every pow_block and output array; the library owns the
  *     device buffers, the HIP stream and the per-template constants.
  *
@@ -128,6 +129,17 @@ int pow_hash_block(pow_ctx* ctx, const pow_block* b, uint8_t digest[32], char he
 int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
              unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
              pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
+
+/* In-flight cancellation (the reference re-checks its chain only after a
+ * trial, node.cpp:315).  Publishes `epoch`, the caller's current value of the
+ * cancel word, to the GPU: a pow_mine / pow_mine_any launch of this ctx whose
+ * `epoch` argument differs stops at its next poll (one inner step, ~60 us)
+ * instead of at its sub-round boundary (up to ~0.13 s), and the call returns 0.
+ * Call it after bumping the cancel word, with its new value, from one thread
+ * at a time.  It is a store into host memory the GPU reads (no HIP call), so
+ * the thread driving the ctx may be inside pow_mine meanwhile.  The first
+ * call arms the GPU-side check for the ctx.  Returns POW_OK. */
+int pow_cancel(pow_ctx* ctx, uint32_t epoch);
 
 /* Lowest-latency form of pow_mine: returns (1) SOME solving counter of the
  * range — the first one the GPU finds; every wave stops at its next step —

@@ -96,6 +96,7 @@ def load() -> ctypes.CDLL:
                        ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, c_sizep], ctypes.c_int),
         "pow_sweep_device": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
                               ctypes.c_void_p, ctypes.c_size_t, c_sizep, c_u64p], ctypes.c_int),
+        "pow_cancel": ([ctypes.c_void_p, ctypes.c_uint32], ctypes.c_int),
         "pow_dev_alloc": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "pow_dev_free": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
         "pow_dev_read": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
@@ -121,7 +122,7 @@ def load() -> ctypes.CDLL:
 
 EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
-           "pow_hash_block", "pow_mine", "pow_mine_any", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
+           "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
            "pow_group_destroy", "pow_group_allreduce_u64", "pow_group_mine")
 

@@ -110,7 +110,12 @@ class Node {
   pow_ctx* recv_ctx_ = nullptr;              // used only by the receive thread
   std::deque<std::pair<pow_block, MPI_Status>> deferred_;
 
-  void bump_epoch() { __atomic_add_fetch(&epoch_, 1u, __ATOMIC_SEQ_CST); }
+  // The chain moved: a running pow_mine_any on the old template stops at its
+  // next GPU poll (pow_cancel), not at its next sub-round (up to ~0.13 s).
+  void bump_epoch() {
+    const uint32_t e = __atomic_add_fetch(&epoch_, 1u, __ATOMIC_SEQ_CST);
+    if (mine_ctx_) pow_cancel(mine_ctx_, e);
+  }
   void set_last(const pow_block* b) {
     last_ = b;
     bump_epoch();
@@ -394,6 +399,7 @@ int Node::run() {
   genesis_.created_at = (uint64_t)time(nullptr);
   last_ = &genesis_;
 
+  pow_cancel(mine_ctx_, epoch_);  // arm the GPU-side epoch check
   std::thread miner([this] {
     pthread_setname_np(pthread_self(), "pow_miner");
     proof_of_work();

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -168,6 +169,11 @@ struct pow_ctx {
   PowBlob* d_blob = nullptr;   // per-template constants + result words, one allocation
   PowBlob* h_blob = nullptr;   // pinned staging copy: uploaded with one H2D per launch
   bool consts_dirty = false;   // h_blob->consts not yet on the device
+  unsigned int* h_epoch = nullptr;      // pow_cancel's word: mapped, coherent host memory ...
+  unsigned int* d_epoch = nullptr;      // ... and its device address
+  std::atomic<bool> armed{false};       // pow_cancel has published an epoch
+  uint32_t launch_epoch = 0;            // mine calls: the caller's epoch ...
+  bool watch_epoch = false;             // ... watched on the GPU when armed
   PowConsts* d_consts = nullptr;  // = &d_blob->consts
   PowResult* d_res = nullptr;     // = &d_blob->res
   PowResult* h_res = nullptr;  // pinned read-back of d_res
@@ -313,6 +319,9 @@ int stage_result(pow_ctx* ctx, bool with_tail) {
   PowResult& r = ctx->h_blob->res;
   memset(&r, 0, sizeof r);
   r.min_rel = ~0ull;
+  r.launch_epoch = ctx->launch_epoch;
+  r.watch_epoch = ctx->watch_epoch && ctx->armed.load(std::memory_order_acquire) ? 1u : 0u;
+  r.host_epoch = ctx->d_epoch;
   if (with_tail) {
     r.tail_buf = ctx->d_tail;
     r.tail_cap = ctx->tail_cap;
@@ -394,6 +403,12 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipEventCreate(&ctx->ev1), "hipEventCreate");
   chk(hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming), "hipEventCreate");
   chk(hipMalloc(&ctx->d_blob, sizeof(PowBlob)), "hipMalloc consts/result");
+  if (ctx->d_blob) chk(hipMemset(ctx->d_blob, 0, sizeof(PowBlob)), "hipMemset");
+  chk(hipHostMalloc(&ctx->h_epoch, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc epoch");
+  if (ctx->h_epoch) {
+    *ctx->h_epoch = 0;
+    chk(hipHostGetDevicePointer((void**)&ctx->d_epoch, ctx->h_epoch, 0), "hipHostGetDevicePointer");
+  }
   chk(hipHostMalloc(&ctx->h_blob, sizeof(PowBlob), hipHostMallocDefault), "hipHostMalloc staging");
   if (ctx->d_blob) {
     ctx->d_consts = &ctx->d_blob->consts;
@@ -427,6 +442,7 @@ void pow_destroy(pow_ctx* ctx) {
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->ev_block) (void)hipEventDestroy(ctx->ev_block);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->h_epoch) (void)hipHostFree(ctx->h_epoch);
   delete ctx;
 }
 
@@ -626,6 +642,12 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   ctx->stats = pow_stats{};
   if (hashes_done) *hashes_done = 0;
   if (int rc = upload_consts(ctx, tmpl)) return rc;
+  ctx->launch_epoch = epoch;
+  ctx->watch_epoch = cancel_word != nullptr;
+  struct Unwatch {  // sweeps and later calls start unwatched
+    pow_ctx* c;
+    ~Unwatch() { c->watch_epoch = false; }
+  } unwatch{ctx};
   // Sub-round plan.
   //  * d <= 21 (expected trials <= 2M): sub-round 1 on the latency kernel K1'
   //    over 16x the expected trials, capped at ctx->lat_max.  Few waves per
@@ -654,6 +676,9 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
       return rc;
     first = false;
     done += n;
+    // cancelled while the launch ran (pow_cancel stops it early; its result,
+    // if any, belongs to a stale template and, in lowest mode, may not be final)
+    if ((cancel_word && *cancel_word != epoch) || ctx->h_res->cancelled) break;
     if (ctx->h_res->min_rel != ~0ull) {
       const PowResult& r = *ctx->h_res;
       const uint64_t ctr = s0 + r.min_rel;
@@ -695,6 +720,15 @@ int pow_mine_any(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64
                  pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
   return mine_impl(ctx, tmpl, ctr_start, ctr_count, diff_bits, cancel_word, epoch, out, found_ctr,
                    hashes_done, true);
+}
+
+int pow_cancel(pow_ctx* ctx, uint32_t epoch) {
+  if (!ctx) return fail(POW_EINVAL, "null");
+  // A plain store into mapped host memory: no HIP call, no stream; the
+  // kernel's sentinel wave reads it over PCIe at its next poll.
+  __atomic_store_n(ctx->h_epoch, epoch, __ATOMIC_SEQ_CST);
+  ctx->armed.store(true, std::memory_order_release);
+  return POW_OK;
 }
 
 int pow_dev_alloc(pow_ctx* ctx, size_t bytes, void** out) {

@@ -114,6 +114,25 @@ __device__ __forceinline__ void flush_tail(const uint32_t* wst, uint32_t nst, ui
   if (lane < nst && base + lane < tail_cap) tail[base + lane] = wst[lane];
 }
 
+// pow_cancel: has the caller's epoch moved past this launch's?  One sentinel
+// wave (workgroup 0, wave 0) reads the caller's epoch from mapped host memory
+// (one PCIe read per poll, so not every wave) and raises res->cancelled; every
+// wave reads that device word.  A memset or copy into device memory could not
+// do this: the copy engine's blit kernel waits for a free CU, and the mining
+// kernel holds them all.  Wave-uniform.
+__device__ __forceinline__ bool epoch_moved(PowResult* res) {
+  if (!res->watch_epoch) return false;
+  if (blockIdx.x == 0 && threadIdx.x < 64u) {
+    const unsigned int now = __hip_atomic_load(res->host_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__builtin_amdgcn_readfirstlane(now) != res->launch_epoch) {
+      if (threadIdx.x == 0) __hip_atomic_store(&res->cancelled, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(
+             __hip_atomic_load(&res->cancelled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+}
+
 // Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
 __device__ __forceinline__ bool full_test(const uint32_t H[8], uint32_t d) {
   uint32_t lz = 0;
@@ -165,6 +184,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       long long lo = (long long)rbase * 62 - (long long)L.off0;
       if (MODE == 2 && f != ~0ull) break;
       if (lo > 0 && f < (unsigned long long)lo) break;
+      if (epoch_moved(res)) break;
     }
     const uint32_t r = rbase + lane;
 
@@ -213,11 +233,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         f = uniform64(f);
         long long lo = (long long)rbase * 62 + j - (long long)L.off0;
         if (lo > 0 && f < (unsigned long long)lo) break;
+        if (epoch_moved(res)) {
+          stop = true;
+          break;
+        }
       }
       if (MODE == 2 && j != 0) {
         unsigned long long f =
             __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (uniform64(f) != ~0ull) {
+        if (uniform64(f) != ~0ull || epoch_moved(res)) {
           stop = true;
           break;
         }
@@ -318,7 +342,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         }
       }
     }
-    if (MODE == 2 && stop) break;
+    if (MODE >= 1 && stop) break;
   }
   if (MODE == 0) {
     if (nst >= 32) flush_stage(wst, nst, lane, res, out, L.cap);
@@ -370,6 +394,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     f = uniform64(f);
     if (ANY ? f != ~0ull : f < (unsigned long long)q) break;
+    if (epoch_moved(res)) break;
     ++iters;
     const uint32_t rel = q + lane;
     uint32_t dg[9];

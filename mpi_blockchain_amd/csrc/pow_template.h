@@ -96,7 +96,11 @@ struct PowResult {
   unsigned int* tail_buf;      // sweep: each wave's last < 32 solutions (appended by the host);
                                // read from here at wave exit, not held in SGPRs all kernel long
   unsigned int nhit;           // latency kernel: solutions found (the first POW_HITS are in hit[])
-  unsigned int pad2;
+  unsigned int launch_epoch;   // mine modes: the caller's epoch for this launch ...
+  unsigned int watch_epoch;    // ... watched when nonzero (pow_cancel armed):
+  const unsigned int* host_epoch;  // the caller's current epoch, in mapped host memory
+  unsigned int cancelled;      // set once a sentinel wave saw host_epoch != launch_epoch
+  unsigned int pad3;
   PowHit hit[POW_HITS];
 };
 

@@ -103,8 +103,12 @@ class GpuMiner:
 
     # ---- mining ----
     def cancel(self) -> None:
-        """Called from another thread (the receive loop) when the chain moved."""
+        """Called from another thread (the receive loop) when the chain moved:
+        bumps the cancel word and publishes it to the GPU (pow_cancel), so a
+        running mine call stops within one inner step, not at its next
+        sub-round."""
         self._cancel.value = (self._cancel.value + 1) & 0xFFFFFFFF
+        check(self.L.pow_cancel(self.ctx, self._cancel.value))
 
     @property
     def epoch(self) -> int:

@@ -67,7 +67,8 @@ def test_no_spills_and_occupancy(isa, variant):
     # SGPRs are capped at 80 (8 workgroups/CU); the few spills this causes sit
     # at chunk-dequeue level and in the rare hit path, never in the j-loop
     # (test_j_loop_clean).
-    assert md["sgpr_spill_count"] <= 16
+    # (mine modes also keep the early-exit / cancellation poll state: <= 24)
+    assert md["sgpr_spill_count"] <= (16 if "ILi0E" in variant else 24)
     assert md["vgpr_spill_count"] == 0
     assert md["private_segment_fixed_size"] == 0
     assert md["vgpr_count"] <= 64, md  # 8 waves / SIMD

@@ -200,6 +200,38 @@ def test_cancel_epoch(miner, templates):
     assert miner.stats()["launches"] == 0
 
 
+@pytest.mark.parametrize("any_solution", [True, False])
+def test_cancel_in_flight(any_solution):
+    """pow_cancel from another thread stops a running mine call within one
+    inner step: a search with no solution (d = 60) over 2^40 counters runs
+    2^30-counter K1 launches of ~0.13 s; cancelled 30 ms in, it returns None
+    within a few ms instead of at the end of its launch."""
+    import threading
+    import time
+
+    b = block_from_template({"index": 5, "node_owner_number": 1, "difficulty": 9, "created_at": 1700000000,
+                             "previous_block_hash_hex": "00" * 256})
+    with GpuMiner(0) as m:
+        m.cancel()  # arm the GPU-side check (first pow_cancel)
+        ep = m.epoch
+        assert m.mine(b, 0, 1 << 26, 60, epoch=ep, any_solution=any_solution) is None  # not cancelled: runs out
+        res, t_end = {}, {}
+
+        def run():
+            res["r"] = m.mine(b, 0, 1 << 40, 60, epoch=ep, any_solution=any_solution)
+            t_end["t"] = time.perf_counter()
+
+        th = threading.Thread(target=run)
+        th.start()
+        time.sleep(0.03)
+        t_cancel = time.perf_counter()
+        m.cancel()
+        th.join(timeout=30)
+        assert not th.is_alive()
+        assert res["r"] is None
+        assert t_end["t"] - t_cancel < 0.02, t_end["t"] - t_cancel  # a 2^30 launch takes ~0.13 s
+
+
 def test_chained_blocks_validate(miner):
     """Mine three chained blocks with the GPU and check the chain the way the
     receive side does (valid_new_block, block.cpp:13-25: recomputed hash ==
