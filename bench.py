@@ -66,8 +66,11 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
                "sample": (f"reference proof_of_work loop body (node.cpp:292-308; /root/reference block.cpp + "
                           f"picosha2.h built -O2 by oracle/Makefile), {procs} processes x {seconds} s, "
                           f"rand() nonces, difficulty 9")}
+        res["per_core"] = round(o2["trials_per_s"] / procs, 1)
         if "O0" in out and "trials_per_s" in out["O0"]:
             res["as_shipped_O0"] = round(out["O0"]["trials_per_s"], 1)
+            res["as_shipped_O0_per_core"] = round(out["O0"]["trials_per_s"] / procs, 1)
+        res["host_cpus"] = {"nproc": os.cpu_count(), "affinity": cores, "used": procs}
         return res
     # restatement fallback ("port")
     try:
