@@ -28,7 +28,7 @@
 //     receive loop polls with a backoff instead of MPICH's spinning probe
 //     (T12: the reference burns a core per rank there).
 //
-//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS]
+//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US]
 #include <mpi.h>
 #include <unistd.h>
 
@@ -66,14 +66,15 @@ struct Options {
   unsigned blocks = 10;     // BLOCKS_TO_MINE (block.h:7)
   int device = -1;          // -1: local rank modulo visible GPUs
   unsigned round_log2 = 32; // counters per pow_mine call
-  unsigned pause_ms = 0;    // sleep before each round (lets slower CPU ranks compete in tests)
+  unsigned pause_us = 0;    // sleep a random 0..pause_us us before each round (tests: lets slower
+                            // CPU ranks compete, and decorrelates GPU ranks so forks happen)
 };
 
 // MPI_Probe that sleeps between polls instead of spinning.  MPICH's blocking
 // probe/receive busy-polls, so every reference rank burns a core in its
 // receive loop on top of its mining thread (node.cpp:404).
 // Here the GPU does the mining, so the receive thread should not take a core:
-// it polls with MPI_Iprobe and backs off from 5 us to 200 us while idle (the
+// it polls with MPI_Iprobe and backs off from 5 us to 50 us while idle (the
 // first polls after a message stay fast, so a burst is served at full speed).
 void probe_any(MPI_Status* st) {
   int flag = 0;
@@ -82,7 +83,7 @@ void probe_any(MPI_Status* st) {
     MPI_Iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, &flag, st);
     if (flag) return;
     std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
-    nap_us = std::min(200u, nap_us * 2);
+    nap_us = std::min(50u, nap_us * 2);
   }
 }
 
@@ -337,7 +338,7 @@ class Node {
       tmpl.difficulty = opt_.difficulty;
       tmpl.created_at = (uint64_t)time(nullptr);
       memcpy(tmpl.previous_block_hash, tmpl.block_hash, POW_HASH_SIZE);
-      if (opt_.pause_ms) std::this_thread::sleep_for(std::chrono::milliseconds(opt_.pause_ms));
+      if (opt_.pause_us) std::this_thread::sleep_for(std::chrono::microseconds(rng() % (opt_.pause_us + 1ull)));
       const uint64_t start = rng() % (POW_COUNTER_LIMIT - round);
       pow_block solved;
       uint64_t ctr = 0;
@@ -443,7 +444,8 @@ int main(int argc, char** argv) {
     else if (k == "--blocks") o.blocks = (unsigned)v;
     else if (k == "--device") o.device = (int)v;
     else if (k == "--round") o.round_log2 = (unsigned)std::min(40l, std::max(12l, v));
-    else if (k == "--pause-ms") o.pause_ms = (unsigned)v;
+    else if (k == "--pause-ms") o.pause_us = (unsigned)v * 1000u;
+    else if (k == "--pause-us") o.pause_us = (unsigned)v;
   }
   Node n(o);
   if (n.init_gpu() != 0) return 1;
