@@ -43,8 +43,8 @@ hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t str
 hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
 hipError_t pow_sort_u32(void* temp, size_t* temp_bytes, uint32_t* keys, uint32_t* alt, uint32_t n,
                         uint32_t** sorted, hipStream_t stream);
-hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConsts* C,
-                                 const PowLaunchLat& L, PowResult* res);
+hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConsts& C,
+                                 const PowLaunchLat& L, PowResult* res, PowResult* hout);
 
 namespace {
 
@@ -169,6 +169,9 @@ struct pow_ctx {
   PowBlob* d_blob = nullptr;   // per-template constants + result words, one allocation
   PowBlob* h_blob = nullptr;   // pinned staging copy: uploaded with one H2D per launch
   bool consts_dirty = false;   // h_blob->consts not yet on the device
+  PowResult* d_lat = nullptr;           // latency kernel: self-resetting device result words ...
+  PowResult* h_lat = nullptr;           // ... published by its last wave here (mapped host memory)
+  PowResult* d_lat_host = nullptr;      // device address of h_lat
   unsigned int* h_epoch = nullptr;      // pow_cancel's word: mapped, coherent host memory ...
   unsigned int* d_epoch = nullptr;      // ... and its device address
   std::atomic<bool> armed{false};       // pow_cancel has published an epoch
@@ -288,16 +291,20 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   L.count = count;
   L.diff = diff;
   L.thr = diff >= 32 ? 0u : (0xFFFFFFFFu >> diff);
-  if (int rc = stage_result(ctx, false)) return rc;
+  L.watch_epoch = ctx->watch_epoch && ctx->armed.load(std::memory_order_acquire) ? 1u : 0u;
+  L.host_epoch = ctx->d_epoch;
+  L.launch_epoch = ctx->launch_epoch;
   // A 256-thread workgroup puts one wave on each SIMD of its CU.
   const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
-  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->d_consts, L,
-                               ctx->d_res));
+  // One dispatch: constants by value (kernarg), result published by the
+  // kernel's last wave into mapped host memory (no copy kernels).
+  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->h_blob->consts, L,
+                               ctx->d_lat, ctx->d_lat_host));
   HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
-  HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  memcpy(ctx->h_res, (const void*)ctx->h_lat, sizeof(PowResult));
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats.kernel_ms += ms;
@@ -387,7 +394,10 @@ int pow_init(int device, pow_ctx** out) {
   ctx->cu_count = prop.multiProcessorCount;
   ctx->clock_khz = prop.clockRate;
   snprintf(ctx->name, sizeof ctx->name, "%s", prop.name);
-  ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u;  // 8 x 256-thread WGs = 32 waves/CU
+  // 8 x 256-thread WGs = 32 waves/CU fill the chip; one slot stays free so
+  // that a K2 launch (block validation on another stream/context, 40 VGPRs)
+  // can run beside a K1 launch instead of waiting up to its whole ~0.13 s.
+  ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u - 1u;
   if (const char* ff = getenv("POW_FORCE_FULL")) ctx->force_full = ff[0] == '1';
   if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
   if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
@@ -404,6 +414,15 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming), "hipEventCreate");
   chk(hipMalloc(&ctx->d_blob, sizeof(PowBlob)), "hipMalloc consts/result");
   if (ctx->d_blob) chk(hipMemset(ctx->d_blob, 0, sizeof(PowBlob)), "hipMemset");
+  chk(hipMalloc(&ctx->d_lat, sizeof(PowResult)), "hipMalloc latency result");
+  chk(hipHostMalloc(&ctx->h_lat, sizeof(PowResult), hipHostMallocMapped | hipHostMallocCoherent),
+      "hipHostMalloc latency result");
+  if (ctx->d_lat && ctx->h_lat) {
+    PowResult init{};
+    init.min_rel = ~0ull;
+    chk(hipMemcpy(ctx->d_lat, &init, sizeof init, hipMemcpyHostToDevice), "hipMemcpy");
+    chk(hipHostGetDevicePointer((void**)&ctx->d_lat_host, ctx->h_lat, 0), "hipHostGetDevicePointer");
+  }
   chk(hipHostMalloc(&ctx->h_epoch, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc epoch");
   if (ctx->h_epoch) {
     *ctx->h_epoch = 0;
@@ -443,6 +462,8 @@ void pow_destroy(pow_ctx* ctx) {
   if (ctx->ev_block) (void)hipEventDestroy(ctx->ev_block);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->h_epoch) (void)hipHostFree(ctx->h_epoch);
+  (void)hipFree(ctx->d_lat);
+  if (ctx->h_lat) (void)hipHostFree(ctx->h_lat);
   delete ctx;
 }
 
@@ -458,7 +479,8 @@ int pow_warmup(pow_ctx* ctx) {
       HIP_OK(pow_launch_search(mode, full != 0, 1, ctx->stream, ctx->d_consts, L, nullptr, ctx->d_res));
   for (int any = 0; any < 2; ++any)
     for (int full = 0; full < 2; ++full)
-      HIP_OK(pow_launch_search_lat(full != 0, any != 0, 1, ctx->stream, ctx->d_consts, LL, ctx->d_res));
+      HIP_OK(pow_launch_search_lat(full != 0, any != 0, 1, ctx->stream, ctx->h_blob->consts, LL, ctx->d_lat,
+                                   ctx->d_lat_host));
   HIP_OK(pow_launch_hash(0, ctx->stream, nullptr, nullptr));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   pow_block b;
@@ -681,15 +703,19 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
     if ((cancel_word && *cancel_word != epoch) || ctx->h_res->cancelled) break;
     if (ctx->h_res->min_rel != ~0ull) {
       const PowResult& r = *ctx->h_res;
-      const uint64_t ctr = s0 + r.min_rel;
+      // The latency kernel records its first POW_HITS hits with their digests.
+      // pow_mine needs the lowest hit (min_rel); pow_mine_any takes the lowest
+      // RECORDED hit, so at low d (more hits per launch than slots) it still
+      // needs no K2 launch.  Otherwise K2 hashes the winner.
+      const PowHit* h = nullptr;
+      for (uint32_t k = 0; lat && k < std::min<uint32_t>(r.nhit, POW_HITS); ++k) {
+        const PowHit* c = &r.hit[k];
+        if (any ? (!h || c->rel < h->rel) : c->rel == r.min_rel) h = c;
+      }
+      const uint64_t ctr = s0 + (h ? h->rel : r.min_rel);
       *out = *tmpl;
       pow_nonce_from_counter(ctr, out->nonce);
       char hx[65];
-      // The latency kernel records its hits with their digests; otherwise (or
-      // if the winner was not among the first POW_HITS) K2 hashes the winner.
-      const PowHit* h = nullptr;
-      for (uint32_t k = 0; lat && k < std::min<uint32_t>(r.nhit, POW_HITS); ++k)
-        if (r.hit[k].rel == r.min_rel) h = &r.hit[k];
       if (h) {
         digest_out(h->digest, nullptr, hx);
       } else {

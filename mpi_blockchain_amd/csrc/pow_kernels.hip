@@ -120,17 +120,21 @@ __device__ __forceinline__ void flush_tail(const uint32_t* wst, uint32_t nst, ui
 // wave reads that device word.  A memset or copy into device memory could not
 // do this: the copy engine's blit kernel waits for a free CU, and the mining
 // kernel holds them all.  Wave-uniform.
-__device__ __forceinline__ bool epoch_moved(PowResult* res) {
-  if (!res->watch_epoch) return false;
+__device__ __forceinline__ bool epoch_moved(uint32_t watch, const unsigned int* host_epoch, uint32_t launch_epoch,
+                                            unsigned int* cancelled) {
+  if (!watch) return false;
   if (blockIdx.x == 0 && threadIdx.x < 64u) {
-    const unsigned int now = __hip_atomic_load(res->host_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (__builtin_amdgcn_readfirstlane(now) != res->launch_epoch) {
-      if (threadIdx.x == 0) __hip_atomic_store(&res->cancelled, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int now = __hip_atomic_load(host_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__builtin_amdgcn_readfirstlane(now) != launch_epoch) {
+      if (threadIdx.x == 0) __hip_atomic_store(cancelled, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return true;
     }
   }
   return __builtin_amdgcn_readfirstlane(
-             __hip_atomic_load(&res->cancelled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+             __hip_atomic_load(cancelled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+}
+__device__ __forceinline__ bool epoch_moved(PowResult* res) {
+  return epoch_moved(res->watch_epoch, res->host_epoch, res->launch_epoch, &res->cancelled);
 }
 
 // Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
@@ -379,14 +383,26 @@ template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32
 // per us) would itself bound the rate.  K1 instead keeps the lowest
 // prefixes' wave busy for all 62 values of the last digit (~0.6 ms on an idle
 // SIMD).  Costs ~8% more VALU per trial than K1 (no j-uniform terms).
+//
+// Launch overhead matters at this size (~17 us of kernel at d = 9), so the
+// constants travel as a by-value kernel argument (kernarg segment, read by
+// scalar loads like any constant) instead of a separate H2D copy, the device
+// result words `res` reset themselves (the last wave to exit re-initialises
+// them), and that last wave also copies them to `hout`, mapped host memory:
+// a launch is one dispatch and no copy kernels.
 template <bool FULL, bool ANY>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search_lat(
-    const PowConsts* __restrict__ C, PowLaunchLat L, PowResult* __restrict__ res) {
+    const PowConsts C0, PowLaunchLat L, PowResult* __restrict__ res, PowResult* __restrict__ hout) {
+  (void)C0;
+  // C0 is the first kernel argument, at offset 0 of the kernarg segment: read
+  // it through that (constant address space) pointer.  Taking C0's address
+  // would make the compiler copy 2.3 KB into private memory per lane.
+  const cptr Cb = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
   uint32_t iters = 0;
-  cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
+  bool wrote_hit = false;  // this wave wrote a hit record (wave-uniform after each step)
   for (unsigned long long qq = (unsigned long long)wave * 64u; qq < L.count;
        qq += (unsigned long long)nwaves * 64u) {
     const uint32_t q = (uint32_t)qq;
@@ -394,7 +410,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     f = uniform64(f);
     if (ANY ? f != ~0ull : f < (unsigned long long)q) break;
-    if (epoch_moved(res)) break;
+    if (epoch_moved(L.watch_epoch, L.host_epoch, L.launch_epoch, &res->cancelled)) break;
     ++iters;
     const uint32_t rel = q + lane;
     uint32_t dg[9];
@@ -440,12 +456,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk(t, as_const(C->kw[c]), H[0]);
+      const_chunk(t, Cb + 64 * c, H[0]);  // PowConsts::kw[c]
       H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
       H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
     }
     St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-    const_chunk(t, as_const(C->kw[3]), H[0]);
+    const_chunk(t, Cb + 64 * 3, H[0]);
     // The whole digest stays live here (this kernel runs at <= 4 waves/SIMD,
     // so the 7 extra VGPRs cost no residency): a hit records it, and the
     // winner's block_hash needs no K2 launch (one serial SHA-256 of 5 chunks
@@ -462,19 +478,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
 #pragma unroll
         for (int k = 0; k < 8; ++k) res->hit[slot].digest[k] = D[k];
       }
+      wrote_hit = true;
     }
+    wrote_hit = __builtin_amdgcn_readfirstlane(__ballot(wrote_hit) != 0ull);
   }
   if (lane == 0) atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);
+  // Last wave out: publish the result to host memory and reset `res` for the
+  // next launch (`next` counts the waves that have exited).  Only waves that
+  // wrote hit records release them (an agent-scope release writes back L2; at
+  // 1,000+ waves per launch that would cost more than the search); min_rel,
+  // hashes and nhit are atomics.  The last wave acquires.
+  if (wrote_hit) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  uint32_t rank = 0;
+  if (lane == 0) rank = __hip_atomic_fetch_add(&res->next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  rank = __builtin_amdgcn_readfirstlane(rank);
+  if (rank == nwaves - 1u) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t nh = res->nhit < POW_HITS ? res->nhit : POW_HITS;
+    if (lane < nh) {  // one lane per recorded hit
+      hout->hit[lane].rel = res->hit[lane].rel;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) hout->hit[lane].digest[k] = res->hit[lane].digest[k];
+    }
+    if (lane == 0) {
+      hout->min_rel = res->min_rel;
+      hout->hashes = res->hashes;
+      hout->nhit = res->nhit;
+      hout->cancelled = res->cancelled;
+      res->min_rel = ~0ull;
+      res->hashes = 0;
+      res->nhit = 0;
+      res->cancelled = 0;
+      res->next = 0;
+    }
+    __threadfence_system();
+  }
 }
 
-template __global__ void pow_search_lat<false, false>(const PowConsts*, PowLaunchLat, PowResult*);
-template __global__ void pow_search_lat<true, false>(const PowConsts*, PowLaunchLat, PowResult*);
-template __global__ void pow_search_lat<false, true>(const PowConsts*, PowLaunchLat, PowResult*);
-template __global__ void pow_search_lat<true, true>(const PowConsts*, PowLaunchLat, PowResult*);
+template __global__ void pow_search_lat<false, false>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, false>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, true>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, true>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
 
 // K2: block_to_hash for n blocks; `msgs` holds each block's 270-byte message
 // already padded on the host to 320 bytes (80 big-endian words).
-__global__ __launch_bounds__(64) void pow_hash_kernel(const uint32_t* __restrict__ msgs, uint32_t n,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void pow_hash_kernel(const uint32_t* __restrict__ msgs, uint32_t n,
                                                       uint32_t* __restrict__ digests) {
   const uint32_t i = blockIdx.x * 64u + threadIdx.x;
   if (i >= n) return;
@@ -482,6 +530,7 @@ __global__ __launch_bounds__(64) void pow_hash_kernel(const uint32_t* __restrict
 #pragma unroll
   for (int k = 0; k < 8; ++k) h[k] = IV[k];
   const uint32_t* m = msgs + (size_t)i * 80u;
+#pragma unroll 1
   for (int c = 0; c < 5; ++c) {
     uint32_t w[16];
 #pragma unroll
@@ -507,12 +556,13 @@ extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hi
 }
 
 extern "C++" hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream,
-                                              const PowConsts* C, const PowLaunchLat& L, PowResult* res) {
+                                              const PowConsts& C, const PowLaunchLat& L, PowResult* res,
+                                              PowResult* hout) {
   dim3 g(grid), b(256);
-  if (!full && !any) hipLaunchKernelGGL((pow_search_lat<false, false>), g, b, 0, stream, C, L, res);
-  else if (!any) hipLaunchKernelGGL((pow_search_lat<true, false>), g, b, 0, stream, C, L, res);
-  else if (!full) hipLaunchKernelGGL((pow_search_lat<false, true>), g, b, 0, stream, C, L, res);
-  else hipLaunchKernelGGL((pow_search_lat<true, true>), g, b, 0, stream, C, L, res);
+  if (!full && !any) hipLaunchKernelGGL((pow_search_lat<false, false>), g, b, 0, stream, C, L, res, hout);
+  else if (!any) hipLaunchKernelGGL((pow_search_lat<true, false>), g, b, 0, stream, C, L, res, hout);
+  else if (!full) hipLaunchKernelGGL((pow_search_lat<false, true>), g, b, 0, stream, C, L, res, hout);
+  else hipLaunchKernelGGL((pow_search_lat<true, true>), g, b, 0, stream, C, L, res, hout);
   return hipGetLastError();
 }
 

@@ -62,8 +62,11 @@ struct PowLaunchLat {
   uint32_t base_digit[9];  // base-62 digits of ctr_start (nonce[0..8])
   uint32_t thr;            // as PowLaunch
   uint32_t diff;
-  uint32_t pad;
+  uint32_t watch_epoch;    // pow_cancel armed: watch host_epoch against launch_epoch
   uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
+  const unsigned int* host_epoch;
+  uint32_t launch_epoch;
+  uint32_t pad;
 };
 
 struct PowLaunch {

@@ -67,17 +67,23 @@ __device__ __forceinline__ void round_k_w(St& s, uint32_t k, uint32_t w) {
   s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
 }
 
-// Generic compression of one chunk with an in-register schedule (used by the
-// single-hash kernel K2; not on the mining hot loop).
+// Generic compression of one chunk (used by the single-hash kernel K2; not on
+// the mining hot loop).  The schedule is a 16-word ring computed just ahead
+// of its round, so K2 stays within 64 VGPRs: it must fit beside a running K1
+// (one workgroup slot is left free for it, pow_api.cpp grid_for).
 __device__ __forceinline__ void compress(uint32_t h[8], const uint32_t win[16]) {
-  uint32_t w[64];
+  uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = win[i];
-#pragma unroll
-  for (int i = 16; i < 64; ++i) w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
   St s{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+#pragma unroll 1
+  for (int r = 0; r < 4; ++r) {  // 4 x 16 rounds; ring indices are constants inside
 #pragma unroll
-  for (int i = 0; i < 64; ++i) round_k_w(s, K[i], w[i]);
+    for (int k = 0; k < 16; ++k) {
+      if (r > 0) w[k] = ssig1(w[(k + 14) & 15]) + w[(k + 9) & 15] + ssig0(w[(k + 1) & 15]) + w[k];
+      round_k_w(s, K[16 * r + k], w[k]);
+    }
+  }
   h[0] += s.a; h[1] += s.b; h[2] += s.c; h[3] += s.d;
   h[4] += s.e; h[5] += s.f; h[6] += s.g; h[7] += s.h;
 }

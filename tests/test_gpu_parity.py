@@ -232,6 +232,33 @@ def test_cancel_in_flight(any_solution):
         assert t_end["t"] - t_cancel < 0.02, t_end["t"] - t_cancel  # a 2^30 launch takes ~0.13 s
 
 
+def test_validation_beside_mining():
+    """Block validation (K2, another context and stream) while a K1 mining
+    launch holds the GPU: K1 leaves one workgroup slot free, so a hash
+    returns in well under a millisecond, not after the ~0.13 s launch."""
+    import statistics
+    import threading
+    import time
+
+    b = block_from_template({"index": 5, "node_owner_number": 1, "difficulty": 9, "created_at": 1700000000,
+                             "previous_block_hash_hex": "00" * 256})
+    with GpuMiner(0) as m, GpuMiner(0) as v:
+        m.cancel()  # arm in-flight cancellation
+        want = v.block_to_hash(b)
+        th = threading.Thread(target=lambda: m.mine(b, 0, 1 << 40, 60, any_solution=True))
+        th.start()
+        time.sleep(0.05)
+        lat = []
+        for _ in range(20):
+            t = time.perf_counter()
+            assert v.block_to_hash(b) == want
+            lat.append(time.perf_counter() - t)
+        m.cancel()
+        th.join(timeout=30)
+        assert not th.is_alive()
+        assert statistics.median(lat) < 0.005, lat
+
+
 def test_chained_blocks_validate(miner):
     """Mine three chained blocks with the GPU and check the chain the way the
     receive side does (valid_new_block, block.cpp:13-25: recomputed hash ==

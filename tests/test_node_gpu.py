@@ -43,10 +43,10 @@ def test_gpu_network(tmp_path, np_, d):
     # At d = 5 a block takes ~50 us on the GPU, and pow_cancel stops a rank's
     # stale search as soon as a block arrives: the last block's finder starts
     # the next round ~0.1 ms before anyone else and wins every block.  A random
-    # 0-300 us pause before each round spreads the starts about as widely as
-    # the message latency, so ranks often finish the same index before hearing
-    # of each other's block (forks).
-    extra = ("--pause-us", "300") if d <= 5 else ()
+    # 0-600 us pause before each round spreads the starts a few message
+    # latencies wide, so ranks often finish the same index before hearing of
+    # each other's block (forks), while receivers keep up with the chain.
+    extra = ("--pause-us", "600") if d <= 5 else ()
     run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240, extra_args=extra)
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout
