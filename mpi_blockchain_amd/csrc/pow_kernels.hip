@@ -386,7 +386,8 @@ template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32
 //
 // Launch overhead matters at this size (~17 us of kernel at d = 9), so the
 // constants travel as a by-value kernel argument (kernarg segment, read by
-// scalar loads like any constant) instead of a separate H2D copy, the device
+// scalar loads like any constant) instead of a separate H2D copy for small
+// grids (L.consts_dev == null), the device
 // result words `res` reset themselves (the last wave to exit re-initialises
 // them), and that last wave also copies them to `hout`, mapped host memory:
 // a launch is one dispatch and no copy kernels.
@@ -397,12 +398,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   // C0 is the first kernel argument, at offset 0 of the kernarg segment: read
   // it through that (constant address space) pointer.  Taking C0's address
   // would make the compiler copy 2.3 KB into private memory per lane.
-  const cptr Cb = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+  // Small grids read the kernarg copy (no H2D copy before the launch); large
+  // ones a device copy: kernarg memory is slower to fetch when hundreds of CUs
+  // miss on it at once (d = 13, 256 workgroups: +7 us).
+  const cptr Cb = L.consts_dev ? as_const(reinterpret_cast<const uint32_t*>(L.consts_dev))
+                               : (cptr)__builtin_amdgcn_kernarg_segment_ptr();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
   uint32_t iters = 0;
   bool wrote_hit = false;  // this wave wrote a hit record (wave-uniform after each step)
+  __shared__ uint32_t wg_iters;  // wave-iterations of this workgroup
+  if (threadIdx.x == 0) wg_iters = 0;
+  __syncthreads();
   for (unsigned long long qq = (unsigned long long)wave * 64u; qq < L.count;
        qq += (unsigned long long)nwaves * 64u) {
     const uint32_t q = (uint32_t)qq;
@@ -482,36 +490,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     }
     wrote_hit = __builtin_amdgcn_readfirstlane(__ballot(wrote_hit) != 0ull);
   }
-  if (lane == 0) atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);
-  // Last wave out: publish the result to host memory and reset `res` for the
-  // next launch (`next` counts the waves that have exited).  Only waves that
-  // wrote hit records release them (an agent-scope release writes back L2; at
-  // 1,000+ waves per launch that would cost more than the search); min_rel,
-  // hashes and nhit are atomics.  The last wave acquires.
+  // Last workgroup out: publish the result to host memory and reset `res`
+  // for the next launch.  One 64-bit atomic per WORKGROUP (its 4 waves sum
+  // their iterations in LDS first) counts both the workgroups that have
+  // exited (low 32 bits) and the wave-iterations done (high 32 bits): at
+  // thousands of waves per launch, per-wave atomics on one address cost tens
+  // of microseconds.  Only waves that wrote hit records release them (an
+  // agent-scope release writes back L2); min_rel and nhit are atomics.  The
+  // last workgroup acquires.
   if (wrote_hit) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  uint32_t rank = 0;
-  if (lane == 0) rank = __hip_atomic_fetch_add(&res->next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  rank = __builtin_amdgcn_readfirstlane(rank);
-  if (rank == nwaves - 1u) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const uint32_t nh = res->nhit < POW_HITS ? res->nhit : POW_HITS;
-    if (lane < nh) {  // one lane per recorded hit
-      hout->hit[lane].rel = res->hit[lane].rel;
+  if (lane == 0) atomicAdd(&wg_iters, iters);
+  __syncthreads();
+  if (threadIdx.x < 64u) {
+    unsigned long long old = 0;
+    if (lane == 0)
+      old = __hip_atomic_fetch_add(&res->hashes, ((unsigned long long)wg_iters << 32) | 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    old = uniform64(old);
+    if ((uint32_t)old == gridDim.x - 1u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const uint32_t nh = res->nhit < POW_HITS ? res->nhit : POW_HITS;
+      if (lane < nh) {  // one lane per recorded hit
+        hout->hit[lane].rel = res->hit[lane].rel;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) hout->hit[lane].digest[k] = res->hit[lane].digest[k];
+        for (int k = 0; k < 8; ++k) hout->hit[lane].digest[k] = res->hit[lane].digest[k];
+      }
+      if (lane == 0) {
+        hout->min_rel = res->min_rel;
+        hout->hashes = ((old >> 32) + wg_iters) * 64ull;
+        hout->nhit = res->nhit;
+        hout->cancelled = res->cancelled;
+        res->min_rel = ~0ull;
+        res->hashes = 0;
+        res->nhit = 0;
+        res->cancelled = 0;
+      }
+      __threadfence_system();
     }
-    if (lane == 0) {
-      hout->min_rel = res->min_rel;
-      hout->hashes = res->hashes;
-      hout->nhit = res->nhit;
-      hout->cancelled = res->cancelled;
-      res->min_rel = ~0ull;
-      res->hashes = 0;
-      res->nhit = 0;
-      res->cancelled = 0;
-      res->next = 0;
-    }
-    __threadfence_system();
   }
 }
 

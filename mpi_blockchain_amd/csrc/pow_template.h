@@ -67,6 +67,7 @@ struct PowLaunchLat {
   const unsigned int* host_epoch;
   uint32_t launch_epoch;
   uint32_t pad;
+  const PowConsts* consts_dev;  // null: read the by-value copy in the kernarg segment
 };
 
 struct PowLaunch {
