@@ -69,19 +69,22 @@ __device__ __forceinline__ void round_k_w(St& s, uint32_t k, uint32_t w) {
 
 // Generic compression of one chunk (used by the single-hash kernel K2; not on
 // the mining hot loop).  The schedule is a 16-word ring computed just ahead
-// of its round, so K2 stays within 64 VGPRs: it must fit beside a running K1
-// (one workgroup slot is left free for it, pow_api.cpp grid_for).
+// of its round, and scheduling barriers every 4 rounds keep the compiler from
+// running the schedule far ahead: K2 stays at 44 VGPRs (it must fit beside a
+// running K1, which leaves one workgroup slot free for it) at the speed of a
+// fully unrolled 78-VGPR version (19.9 us per hash, tools/k2_c.c).
 __device__ __forceinline__ void compress(uint32_t h[8], const uint32_t win[16]) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = win[i];
   St s{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
-#pragma unroll 1
-  for (int r = 0; r < 4; ++r) {  // 4 x 16 rounds; ring indices are constants inside
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // 4 x 16 rounds; ring indices are constants
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       if (r > 0) w[k] = ssig1(w[(k + 14) & 15]) + w[(k + 9) & 15] + ssig0(w[(k + 1) & 15]) + w[k];
       round_k_w(s, K[16 * r + k], w[k]);
+      if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // keep the schedule from running ahead
     }
   }
   h[0] += s.a; h[1] += s.b; h[2] += s.c; h[3] += s.d;
