@@ -88,3 +88,20 @@ def test_j_loop_clean(isa, variant):
     words = sum({"s_load_dwordx16": 16, "s_load_dwordx8": 8, "s_load_dwordx4": 4, "s_load_dwordx2": 2,
                  "s_load_dword": 1}.get(o, 0) for o in ops)
     assert words >= 256, words
+
+
+def test_k2_fits_beside_k1(isa):
+    """K2 (block validation) must fit in the one workgroup slot K1 leaves free
+    (pow_api.cpp: grid = 8 x CUs - 1): a SIMD then has 512 - 7 x 64 = 64 VGPRs
+    for it.  No scratch either."""
+    md = metadata(isa, "_Z15pow_hash_kernel")
+    assert md["vgpr_count"] <= 64, md
+    assert md["vgpr_spill_count"] == 0 and md["private_segment_fixed_size"] == 0, md
+
+
+@pytest.mark.parametrize("variant", ["_Z14pow_search_latILb0ELb0E", "_Z14pow_search_latILb0ELb1E"])
+def test_latency_kernel_no_private_copy(isa, variant):
+    """The latency kernel reads its by-value constants through the kernarg
+    pointer; taking the parameter's address would copy 2.3 KB to scratch."""
+    md = metadata(isa, variant)
+    assert md["private_segment_fixed_size"] == 0 and md["vgpr_spill_count"] == 0, md
