@@ -728,9 +728,16 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
       if (h) {
         digest_out(h->digest, nullptr, hx);
       } else {
+        // Hash the winner with a one-counter K1' launch (difficulty 0: it
+        // records its digest): one dispatch with the constants as kernel
+        // argument, about half the latency of K2's copy-in / hash / copy-out.
         const pow_stats keep = ctx->stats;
-        if (int rc = pow_hash_blocks(ctx, out, 1, nullptr, hx)) return rc;
+        ctx->watch_epoch = false;  // the winner is hashed even if the epoch moves now
+        if (int rc = run_search_lat(ctx, ctr, 1, 0, true, 1)) return rc;
         ctx->stats = keep;
+        const PowResult& w = *ctx->h_res;
+        if (w.nhit < 1 || w.hit[0].rel != 0) return fail(POW_EHIP, "winner re-hash recorded no digest");
+        digest_out(w.hit[0].digest, nullptr, hx);
       }
       memcpy(out->block_hash, hx, 65);  // strcpy semantics (node.cpp:318)
       if (found_ctr) *found_ctr = ctr;
