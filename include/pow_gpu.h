@@ -196,8 +196,9 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
 void pow_group_destroy(pow_group* g);
 /* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream. */
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);
-/* pow_mine over all ranks: rounds of `round_size` counters (0 = 2^30 per
- * rank), each split into static shards; each rank mines the lowest solving
+/* pow_mine over all ranks: rounds of `round_size` counters (0 = adaptive:
+ * ~4x the expected trials first, then 4x larger up to 2^30 per rank), each
+ * split into static shards; each rank mines the lowest solving
  * counter of its shard, then one 24-byte ncclAllReduce(ncclMin) per round
  * picks the winner, spreads cancellation (any rank whose cancel word moved
  * stops every rank: returns 0) and failures (every rank returns < 0).  On 1 the

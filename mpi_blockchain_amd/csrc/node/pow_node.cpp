@@ -17,8 +17,9 @@
 // What changes:
 //   * mining (node.cpp:292-308): each round refreshes the template exactly as
 //     node.cpp:292-299 and runs pow_mine over a counter range on this rank's
-//     GPU; the receive thread bumps a cancel epoch whenever the chain moves,
-//     which stops the round at its next sub-round boundary;
+//     GPU; the receive thread bumps a cancel epoch whenever the chain moves
+//     and publishes it with pow_cancel, which stops the running launch within
+//     ~0.4 ms;
 //   * hardening: while waiting for a TAG_CHAIN_RESPONSE
 //     the receive thread keeps serving TAG_CHAIN_HASH requests and defers
 //     TAG_NEW_BLOCK messages, so two ranks asking each other cannot deadlock
@@ -28,7 +29,7 @@
 //     receive loop polls with a backoff instead of MPICH's spinning probe
 //     (T12: the reference burns a core per rank there).
 //
-//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US]
+//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US] [--winner-pause-us US]
 #include <mpi.h>
 #include <unistd.h>
 
@@ -66,6 +67,8 @@ struct Options {
   unsigned blocks = 10;     // BLOCKS_TO_MINE (block.h:7)
   int device = -1;          // -1: local rank modulo visible GPUs
   unsigned round_log2 = 32; // counters per pow_mine call
+  unsigned winner_pause_us = 0;  // tests: sleep after mining a block (GPU blocks take ~35 us, so
+                                // the last finder would otherwise start every race first)
   unsigned pause_us = 0;    // sleep a random 0..pause_us us before each round (tests: lets slower
                             // CPU ranks compete, and decorrelates GPU ranks so forks happen)
 };
@@ -358,6 +361,9 @@ class Node {
           send_block_to_everyone(*last_);
         }
       }
+      // Tests: let the other ranks receive this block before racing on the next.
+      if (rc == 1 && opt_.winner_pause_us)
+        std::this_thread::sleep_for(std::chrono::microseconds(opt_.winner_pause_us));
     }
     MPI_Abort(MPI_COMM_WORLD, 0);  // node.cpp:330
   }
@@ -446,6 +452,7 @@ int main(int argc, char** argv) {
     else if (k == "--round") o.round_log2 = (unsigned)std::min(40l, std::max(12l, v));
     else if (k == "--pause-ms") o.pause_us = (unsigned)v * 1000u;
     else if (k == "--pause-us") o.pause_us = (unsigned)v;
+    else if (k == "--winner-pause-us") o.winner_pause_us = (unsigned)v;
   }
   Node n(o);
   if (n.init_gpu() != 0) return 1;

@@ -189,9 +189,18 @@ int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint
   if (ctr_start >= POW_COUNTER_LIMIT || ctr_count > POW_COUNTER_LIMIT - ctr_start)
     return pow_set_error(POW_EINVAL, "counter range past 62^9");
   if (diff_bits > 256) return pow_set_error(POW_EINVAL, "difficulty > 256 bits");
-  // Default round: 2^30 counters per GPU (~0.13 s at 8 G/s), so the one
-  // all-reduce per round (tens of microseconds) costs well under 1%.
-  if (round_size == 0) round_size = (uint64_t)g->nranks << 30;
+  // Default (round_size = 0): adaptive rounds, as pow_mine's sub-rounds.  The
+  // first round covers ~4x the expected trials (2^(d+2) counters, at least
+  // 2^16 per GPU), later ones grow 4x up to 2^30 counters per GPU (~0.13 s at
+  // 8 G/s, where the one all-reduce per round costs well under 1%).  A fixed
+  // 2^30 per GPU would make every search take ~0.13 s per round even when the
+  // lowest solution sits in the first milliseconds of rank 0's shard.
+  const uint64_t big = (uint64_t)g->nranks << 30;
+  const bool adaptive = round_size == 0;
+  if (adaptive) {
+    const unsigned dcap = diff_bits > 40 ? 40 : diff_bits;
+    round_size = std::min<uint64_t>(big, std::max<uint64_t>((uint64_t)g->nranks << 16, 1ull << (dcap + 2)));
+  }
   uint64_t hashes = 0;
   if (hashes_done) *hashes_done = 0;
   for (uint64_t done = 0; done < ctr_count;) {
@@ -229,6 +238,7 @@ int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint
       return 1;
     }
     done += n;
+    if (adaptive) round_size = std::min<uint64_t>(big, round_size * 4);
   }
   return 0;
 }

@@ -28,15 +28,28 @@ def partition(start: int, count: int, rank: int, world: int) -> tuple[int, int]:
     return lo, base + (1 if rank < extra else 0)
 
 
+def round_plan(world: int, difficulty: int) -> tuple[int, int]:
+    """First round size and cap of the adaptive plan (as pow_group_mine):
+    ~4x the expected trials, at least 2^16 per rank; rounds then grow 4x up
+    to 2^30 per rank."""
+    big = world << 30
+    return min(big, max(world << 16, 1 << (min(difficulty, 40) + 2))), big
+
+
 def sharded_mine(search: Callable[[int, int], Optional[int]],
                  allreduce_min: Callable[[int], int],
-                 start: int, count: int, round_size: int, rank: int, world: int) -> Optional[int]:
+                 start: int, count: int, round_size: int, rank: int, world: int,
+                 difficulty: int = 0) -> Optional[int]:
     """Lowest solving counter of [start, start+count) over all ranks.
 
     search(s, n)        -> lowest solving counter in [s, s+n) on this rank, or None
     allreduce_min(v)    -> min of v over ranks (v = NONE when nothing found)
+    round_size 0        -> adaptive rounds for `difficulty` (round_plan)
     Every rank returns the same value.
     """
+    adaptive = round_size == 0
+    if adaptive:
+        round_size, big = round_plan(world, difficulty)
     done = 0
     while done < count:
         n = min(round_size, count - done)
@@ -46,6 +59,8 @@ def sharded_mine(search: Callable[[int, int], Optional[int]],
         if best != NONE:
             return best
         done += n
+        if adaptive:
+            round_size = min(big, round_size * 4)
     return None
 
 
@@ -154,9 +169,10 @@ class ShardedMiner:
         self.miner, self.rank, self.world = miner, rank, world
         self.allreduce_min = torch_allreduce_min(device, group)
 
-    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 1 << 31):
+    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0):
         def search(s, n):
             r = self.miner.mine(tmpl, s, n, difficulty)
             return None if r is None else r.counter
 
-        return sharded_mine(search, self.allreduce_min, start, count, round_size, self.rank, self.world)
+        return sharded_mine(search, self.allreduce_min, start, count, round_size, self.rank, self.world,
+                            difficulty)

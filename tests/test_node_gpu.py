@@ -40,13 +40,13 @@ FORK_MSGS = ("Perdí la carrera", "Conflicto suave", "TAG_CHAIN_HASH")
 
 @pytest.mark.parametrize("np_, d", [(4, 9), (6, 5), (8, 5)])  # protocol smoke at d = 5, -np 8
 def test_gpu_network(tmp_path, np_, d):
-    # At d = 5 a block takes ~50 us on the GPU, and pow_cancel stops a rank's
-    # stale search as soon as a block arrives: the last block's finder starts
-    # the next round ~0.1 ms before anyone else and wins every block.  A random
-    # 0-600 us pause before each round spreads the starts a few message
-    # latencies wide, so ranks often finish the same index before hearing of
-    # each other's block (forks), while receivers keep up with the chain.
-    extra = ("--pause-us", "600") if d <= 5 else ()
+    # At d = 5 a block takes ~35 us on the GPU, and pow_cancel stops a rank's
+    # stale search as soon as a block arrives: the last block's finder would
+    # start every next race first and win it.  --winner-pause-us 400 lets the
+    # others receive and validate the block first, and a random 0-200 us pause
+    # per round then makes ranks finish the same index within each other's
+    # message latency (forks).
+    extra = ("--winner-pause-us", "400", "--pause-us", "200") if d <= 5 else ()
     run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240, extra_args=extra)
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout

@@ -81,8 +81,9 @@ def _worker(rank, world, port, q):
     b = make_oblock(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
     red = torch_allreduce_min()
     res = []
-    for start, count, rs, d in ((0, 1 << 12, 1 << 12, 9), (300, 5000, 2048, 9), (0, 40000, 8192, 13)):
-        res.append(sharded_mine(lambda s, n: O.mine(b, s, n, d), red, start, count, rs, rank, world))
+    for start, count, rs, d in ((0, 1 << 12, 1 << 12, 9), (300, 5000, 2048, 9), (0, 40000, 8192, 13),
+                                (0, 40000, 0, 13)):  # rs 0: adaptive rounds (round_plan)
+        res.append(sharded_mine(lambda s, n: O.mine(b, s, n, d), red, start, count, rs, rank, world, d))
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -103,7 +104,7 @@ def test_gloo_world2():
         assert p.exitcode == 0
     O = Oracle()
     b = make_oblock(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
-    want = [O.mine(b, 0, 1 << 12, 9), O.mine(b, 300, 5000, 9), O.mine(b, 0, 40000, 13)]
+    want = [O.mine(b, 0, 1 << 12, 9), O.mine(b, 300, 5000, 9), O.mine(b, 0, 40000, 13), O.mine(b, 0, 40000, 13)]
     assert want[0] == 263  # golden: first S1 solution
     assert out[0] == out[1] == want
 
@@ -136,3 +137,24 @@ def test_group_unique_id_and_arg_checks():
     assert L.pow_group_mine(None, ctypes.byref(blk), 0, 1, 0, 9, None, 0, ctypes.byref(blk), None, None) \
         == _lib.POW_EINVAL
     assert L.pow_group_allreduce_u64(None, None, 0, 0) == _lib.POW_EINVAL
+
+
+def test_round_plan_adaptive():
+    """Adaptive rounds (round_size 0): first round ~4x the expected trials,
+    at least 2^16 per rank, growing 4x up to 2^30 per rank; the winner equals
+    one search over the whole range (multi-rank: test_gloo_world2)."""
+    from mpi_blockchain_amd.shard import round_plan
+
+    assert round_plan(8, 25) == (1 << 27, 8 << 30)
+    assert round_plan(2, 9) == (2 << 16, 2 << 30)
+    assert round_plan(1, 60)[0] == 1 << 30
+    O = Oracle()
+    b = make_oblock(1, 0, 9, 1700000000, b"")
+    for d in (9, 13, 17):
+        sizes = []
+
+        def search(s, n):
+            sizes.append(n)
+            return O.mine(b, s, n, d)
+        assert sharded_mine(search, lambda v: v, 0, 1 << 20, 0, 0, 1, d) == O.mine(b, 0, 1 << 20, d)
+        assert sizes[0] == round_plan(1, d)[0] and all(y == 4 * x for x, y in zip(sizes, sizes[1:-1]))
