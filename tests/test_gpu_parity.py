@@ -294,6 +294,23 @@ def test_full_window_2p32(miner, fingerprints, templates):
         assert mn == lad[d]["first"][0]
 
 
+def test_full_window_2p32_S1(miner, templates):
+    """Config 2 at full size on the second, realistic template S1 (index 7,
+    owner 3, prev = a 64-char hex hash + NUL + zeros): counts and
+    sha256 of the sorted solution list at every rung vs the CPU restatement's
+    fingerprints (tests/golden/fingerprints_2p32_S1.json)."""
+    import json
+
+    fps = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fingerprints_2p32_S1.json")))
+    b = block_from_template(templates["S1"])
+    lad = fps["ladder"]
+    got = miner.sweep(b, 0, 1 << 32, 9, cap=9_000_000)
+    assert got.size == lad["9"]["count"] and fp(got) == lad["9"]["sha256_le_u32"]
+    for d in ("13", "17", "21", "25"):
+        sol = miner.sweep(b, 0, 1 << 32, int(d), cap=lad[d]["count"] + 16)
+        assert sol.size == lad[d]["count"] and fp(sol) == lad[d]["sha256_le_u32"], d
+
+
 def test_mine_full_window_ladder(mminer, fingerprints, templates):
     """pow_mine over S0's [0, 2^32) at every rung (K1' for d <= 21, K1 sub-rounds
     above): the lowest solving counter, then each next one when the search
