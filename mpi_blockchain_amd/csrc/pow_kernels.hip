@@ -360,9 +360,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
     if (lane == 0 && mymin != ~0ull) atomicMin(&res->min_rel, mymin);
   }
   if (MODE >= 1) {
-    // trials computed by this wave (lanes of a wave run the same iterations)
-    if ((threadIdx.x & 63u) == 0)
-      atomicAdd(&res->hashes, (unsigned long long)iters * 64ull);  // j-steps x lanes
+    // Trials computed (lanes of a wave run the same iterations), summed per
+    // workgroup first: after a hit in MODE 2 all ~8,000 waves exit within one
+    // step, and one atomic each on the same address would queue for tens of us.
+    __shared__ uint32_t wave_iters[4];
+    if ((threadIdx.x & 63u) == 0) wave_iters[threadIdx.x >> 6] = iters;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicAdd(&res->hashes,
+                (unsigned long long)(wave_iters[0] + wave_iters[1] + wave_iters[2] + wave_iters[3]) * 64ull);
   }
 }
 
