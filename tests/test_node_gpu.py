@@ -47,7 +47,13 @@ def test_gpu_network(tmp_path, np_, d):
     # per round then makes ranks finish the same index within each other's
     # message latency (forks).
     extra = ("--winner-pause-us", "400", "--pause-us", "200") if d <= 5 else ()
+    import time
+
+    t0 = time.perf_counter()
     run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240, extra_args=extra)
+    if os.environ.get("POW_NODE_LOG_DIR"):  # diagnostics: keep the network's output
+        with open(os.path.join(os.environ["POW_NODE_LOG_DIR"], f"net_{np_}_{d}.log"), "w") as f:
+            f.write(f"wall {time.perf_counter() - t0:.3f} s rc {run.returncode}\n{run.stdout}")
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout
     complete = [r for r, entries in run.chains.items() if check_chain(entries, 10, d)]
