@@ -191,8 +191,17 @@ def main():
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or os.environ.get("BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # BENCH_REHEARSAL=1 (tests only): several ranks share the visible
+        # GPU(s) and talk over gloo, to exercise the N > 1 path on a one-GPU
+        # box (RCCL refuses two ranks on one device).  The numbers it prints
+        # are not a scaling measurement.
+        if os.environ.get("BENCH_REHEARSAL") == "1":
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
 
@@ -242,7 +251,8 @@ def main():
         buf.free()
         dist.destroy_process_group()
         return
-    collective = "rccl all_reduce(min,sum) per step" if dist is not None else "none (single process)"
+    collective = (f"{'rccl' if dist.get_backend() == 'nccl' else dist.get_backend()} all_reduce(min,sum) per step"
+                  if dist is not None else "none (single process)")
 
     kms = statistics.mean(kernel_ms) if kernel_ms else float("nan")
     value = world * WINDOW * args.steps / el
