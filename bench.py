@@ -217,9 +217,12 @@ def main():
 
     kernel_ms = []
 
+    local_last = [None]  # this rank's (solutions, lowest counter) of the last step
+
     def step():
         n, mn = miner.sweep_count(tmpl, start, WINDOW, d, dev_out=buf, cap=cap)
         kernel_ms.append(miner.stats()["kernel_ms"])
+        local_last[0] = (n, mn)
         if dist is not None:
             red[0] = mn if mn is not None else (1 << 63) - 1
             dist.all_reduce(red[0:1], op=dist.ReduceOp.MIN)
@@ -247,6 +250,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
+    # Per-rank parity (outside the timed region): every rank's window whose
+    # fingerprints are committed (rank 0: [0, 2^32); rank 7: [7*2^32, 8*2^32),
+    # the farthest window of an 8-GPU run) is checked against them.
+    per_rank = [local_last[0]]
+    if dist is not None:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, local_last[0])
     if rank != 0:
         buf.free()
         dist.destroy_process_group()
@@ -267,12 +277,18 @@ def main():
         if miner.L.pow_valu_peak(local, ctypes.byref(lo), ctypes.byref(ms)) == 0:
             peak["microbench_tops"] = round(lo.value / 1e12, 2)
     # sanity/parity at full size: rank 0's window is the golden 2^32 window
-    parity = {"solutions_rank0": last[0] if world == 1 else None, "lowest": last[1]}
-    fpp = os.path.join(ROOT, "tests", "golden", "fingerprints_2p32.json")
-    if world == 1 and os.path.exists(fpp) and d == 9:
-        want = json.load(open(fpp))["ladder"]["9"]
-        parity["expected"] = want["count"]
-        parity["count_ok"] = last[0] == want["count"] and last[1] == want["first"][0]
+    parity = {"solutions_rank0": per_rank[0][0], "solutions_all_ranks": last[0], "lowest": last[1]}
+    checked = {}
+    for r, (n_r, mn_r) in enumerate(per_rank):
+        fpp = os.path.join(ROOT, "tests", "golden",
+                           "fingerprints_2p32.json" if r == 0 else f"fingerprints_2p32_S0_at{r * WINDOW}.json")
+        if d == 9 and os.path.exists(fpp):
+            want = json.load(open(fpp))["ladder"]["9"]
+            checked[str(r)] = {"solutions": n_r, "expected": want["count"],
+                               "ok": n_r == want["count"] and mn_r == r * WINDOW + want["first"][0]}
+    if checked:
+        parity["checked_ranks"] = checked
+        parity["count_ok"] = all(c["ok"] for c in checked.values())
     res = {
         "metric": "SHA-256 nonce trials/sec (whole job) + % int32 VALU peak",
         "value": round(value, 1),

@@ -71,6 +71,7 @@ struct Options {
                                 // the last finder would otherwise start every race first)
   unsigned pause_us = 0;    // sleep a random 0..pause_us us before each round (tests: lets slower
                             // CPU ranks compete, and decorrelates GPU ranks so forks happen)
+  bool serial_init = false; // --serial-init 1: GPU set-up before MPI_Init instead of beside it
 };
 
 // MPI_Probe that sleeps between polls instead of spinning.  MPICH's blocking
@@ -369,11 +370,13 @@ class Node {
   }
 };
 
-// GPU setup runs BEFORE MPI_Init: HIP start-up takes ~1 s, and MPICH's
-// MPI_Init synchronises every process of the job (reference ranks included),
-// so no rank starts mining while a GPU rank is still initialising.  The
-// device is the node-local rank (from the launcher's environment) modulo the
-// visible GPUs.
+// GPU set-up (HIP start-up, 160-220 ms per process, two contexts, kernel
+// warm-up) runs on a thread beside MPI_Init, which itself waits for every
+// process of the job, so a rank's start-up costs the longer of the two rather
+// than their sum.  The miner starts only once both are done.  (--serial-init 1
+// runs it before MPI_Init instead: then no reference rank of a mixed job can
+// start mining while a GPU rank is still initialising.)  The device is the
+// node-local rank (from the launcher's environment) modulo the visible GPUs.
 int Node::init_gpu() {
   int ndev = 0, local = 0;
   if (pow_device_count(&ndev) != POW_OK || ndev < 1) {
@@ -453,14 +456,24 @@ int main(int argc, char** argv) {
     else if (k == "--pause-ms") o.pause_us = (unsigned)v * 1000u;
     else if (k == "--pause-us") o.pause_us = (unsigned)v;
     else if (k == "--winner-pause-us") o.winner_pause_us = (unsigned)v;
+    else if (k == "--serial-init") o.serial_init = v != 0;
   }
   Node n(o);
-  if (n.init_gpu() != 0) return 1;
+  int gpu_rc = 0;
+  std::thread gpu_init;
+  if (o.serial_init) {
+    if (n.init_gpu() != 0) return 1;
+  } else {
+    gpu_init = std::thread([&] { gpu_rc = n.init_gpu(); });
+  }
   int provided = 0;
-  if (MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided) != MPI_SUCCESS) {
+  const int mpi_rc = MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);
+  if (gpu_init.joinable()) gpu_init.join();
+  if (mpi_rc != MPI_SUCCESS) {
     fprintf(stderr, "Error de MPI al inicializar.\n");
     return 1;
   }
+  if (gpu_rc != 0) MPI_Abort(MPI_COMM_WORLD, 1);
   if (provided < MPI_THREAD_MULTIPLE) {  // blockchain.cpp:15 never checks this
     fprintf(stderr, "MPI_THREAD_MULTIPLE not provided (%d)\n", provided);
     MPI_Abort(MPI_COMM_WORLD, 1);

@@ -11,11 +11,13 @@ count; the higher rungs are the subsets with lz >= d.  Cross-checked against the
 independent hashlib computation recorded in SURVEY.md §8c (same counts and
 hashes).  Runtime: ~20 min on 8 cores.
 
-    python tests/golden/gen_fingerprints_2p32.py [threads] [S0|S1]
+    python tests/golden/gen_fingerprints_2p32.py [threads] [S0|S1] [start]
 
 S1 (the realistic chained template of SURVEY.md §8c: index=7, owner=3,
 difficulty=9, created_at=1760572800, prev = a 64-char hex hash + NUL + zeros)
-goes to fingerprints_2p32_S1.json.
+goes to fingerprints_2p32_S1.json.  A non-zero start (e.g. 7 * 2^32: the window
+rank 7 sweeps in bench.py's 8-GPU run) goes to
+fingerprints_2p32_<template>_at<start>.json; counters in it are relative to start.
 """
 import ctypes, hashlib, json, os, sys, time
 
@@ -27,6 +29,7 @@ from oracle.oracle import OBlock, Oracle, make_oblock  # noqa: E402
 
 threads = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 which = sys.argv[2] if len(sys.argv) > 2 else "S0"
+start = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 O = Oracle()
 L = O.L
 L.oracle_sweep_lz.argtypes = [ctypes.POINTER(OBlock), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
@@ -41,16 +44,18 @@ cap = 9_000_000
 ctr = np.zeros(cap, np.uint32)
 lz = np.zeros(cap, np.uint8)
 t = time.time()
-n = L.oracle_sweep_lz(ctypes.byref(S0), 0, 1 << 32, 9, ctr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+n = L.oracle_sweep_lz(ctypes.byref(S0), start, 1 << 32, 9, ctr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
                       lz.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), cap, threads)
 assert n <= cap
 ctr, lz = ctr[:n], lz[:n]
-out = {"template": which, "start": 0, "count": 1 << 32, "seconds": round(time.time() - t, 1), "ladder": {}}
+out = {"template": which, "start": start, "count": 1 << 32, "seconds": round(time.time() - t, 1), "ladder": {}}
 for d in (9, 13, 17, 21, 25):
     sel = ctr[lz >= d]
     out["ladder"][str(d)] = {"count": int(sel.size),
                              "sha256_le_u32": hashlib.sha256(sel.astype("<u4").tobytes()).hexdigest(),
                              "first": [int(x) for x in sel[:8]]}
 name = "fingerprints_2p32.json" if which == "S0" else f"fingerprints_2p32_{which}.json"
+if start:
+    name = f"fingerprints_2p32_{which}_at{start}.json"
 json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), name), "w"), indent=1)
 print(json.dumps(out))

@@ -31,11 +31,10 @@ def test_bench_json_contract():
     assert d["parity"]["count_ok"] is True
 
 
-def test_bench_multi_rank_rehearsal():
-    """The N > 1 path as the driver launches it (torch.distributed.run, one
-    rank per GPU), rehearsed with 2 ranks sharing this box's GPU over gloo
-    (BENCH_REHEARSAL=1; RCCL refuses two ranks on one device): rank 0 prints
-    ONE JSON line with n_gpus = 2 and the whole-job value."""
+def run_rehearsal(n: int) -> dict:
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run,
+    one rank per GPU), rehearsed with n ranks sharing this box's GPU over gloo
+    (BENCH_REHEARSAL=1; RCCL refuses two ranks on one device)."""
     import socket
 
     s = socket.socket()
@@ -43,14 +42,35 @@ def test_bench_multi_rank_rehearsal():
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, BENCH_REHEARSAL="1")
-    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                         "--master-addr", "127.0.0.1", "--master-port", str(port),
-                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1"],
+                        os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "1", "--warmup", "1"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 1e9
+    assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 1e9
     assert "gloo all_reduce" in d["config"]["parallelism"]
     assert "cpu_baseline" not in d and "ladder" not in d  # rank-0-at-N=1-only extras
+    return d
+
+
+def test_bench_multi_rank_rehearsal():
+    """2 ranks: rank 0 prints ONE JSON line with n_gpus = 2, the whole-job
+    value, and rank 0's window checked against its fingerprints."""
+    d = run_rehearsal(2)
+    assert d["parity"]["checked_ranks"]["0"]["ok"] is True and d["parity"]["count_ok"] is True
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "tests", "golden",
+                                                    "fingerprints_2p32_S0_at30064771072.json")),
+                    reason="rank-7 window fingerprints not generated")
+def test_bench_eight_rank_rehearsal():
+    """The driver's 8-GPU launch shape (8 ranks; here sharing one GPU): every
+    rank sweeps its own 2^32 window, the job total is the sum, and rank 7's
+    window [7*2^32, 8*2^32) matches the CPU restatement's fingerprints."""
+    d = run_rehearsal(8)
+    chk = d["parity"]["checked_ranks"]
+    assert chk["0"]["ok"] is True and chk["7"]["ok"] is True and d["parity"]["count_ok"] is True
+    assert d["parity"]["solutions_all_ranks"] > 8 * 8_000_000

@@ -311,6 +311,29 @@ def test_full_window_2p32_S1(miner, templates):
         assert sol.size == lad[d]["count"] and fp(sol) == lad[d]["sha256_le_u32"], d
 
 
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "golden",
+                                                    "fingerprints_2p32_S0_at30064771072.json")),
+                    reason="rank-7 window fingerprints not generated")
+def test_full_window_2p32_far(miner, templates):
+    """S0 over [7*2^32, 8*2^32): the window rank 7 sweeps in bench.py's 8-GPU
+    run (nonce digit 2 no longer 'a', counters past 2^32 in the launch base).
+    Counts, sha256 of the sorted list (relative counters) and lowest counter
+    at every rung vs the CPU restatement (tests/golden/gen_fingerprints_2p32.py)."""
+    import json
+
+    start = 7 << 32
+    fps = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                      f"fingerprints_2p32_S0_at{start}.json")))
+    assert fps["start"] == start
+    b = block_from_template(templates["S0"])
+    lad = fps["ladder"]
+    got = miner.sweep(b, start, 1 << 32, 9, cap=9_000_000)
+    assert got.size == lad["9"]["count"] and fp(got) == lad["9"]["sha256_le_u32"]
+    for d in ("13", "17", "21", "25"):
+        n, mn = miner.sweep_count(b, start, 1 << 32, int(d))
+        assert n == lad[d]["count"] and mn == start + lad[d]["first"][0], d
+
+
 def test_mine_full_window_ladder(mminer, fingerprints, templates):
     """pow_mine over S0's [0, 2^32) at every rung (K1' for d <= 21, K1 sub-rounds
     above): the lowest solving counter, then each next one when the search
