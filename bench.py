@@ -129,6 +129,15 @@ def protocol_runs() -> dict:
                 out[f"gpu_np4_d{d}_wall_s"] = round(time.perf_counter() - t, 3)
                 out[f"gpu_np4_d{d}_rc"] = run.returncode
                 out[f"gpu_np4_d{d}_chains"] = len(run.chains)
+        # The reference's own published experiment closest to real mining
+        # (d = 18, 3 nodes, 10 blocks, median 44.831 s on
+        # unstated hardware); tools/published_replay.py replays the whole table.
+        with tempfile.TemporaryDirectory() as td:
+            t = time.perf_counter()
+            run = run_network(3, td, difficulty=18, blocks=10, timeout=180)
+            out["gpu_np3_d18_wall_s"] = round(time.perf_counter() - t, 3)
+            out["gpu_np3_d18_rc"] = run.returncode
+            out["reference_published_np3_d18_wall_s"] = 44.831
     except Exception as e:  # pragma: no cover
         out["error"] = str(e)
     return out
