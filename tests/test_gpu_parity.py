@@ -316,7 +316,7 @@ def test_full_window_2p32_S1(miner, templates):
                     reason="rank-7 window fingerprints not generated")
 def test_full_window_2p32_far(miner, templates):
     """S0 over [7*2^32, 8*2^32): the window rank 7 sweeps in bench.py's 8-GPU
-    run (nonce digit 2 no longer 'a', counters past 2^32 in the launch base).
+    run (nonce[3] = 'G'..'L' instead of 'a'..'e', counters past 2^32 in the launch base).
     Counts, sha256 of the sorted list (relative counters) and lowest counter
     at every rung vs the CPU restatement (tests/golden/gen_fingerprints_2p32.py)."""
     import json
