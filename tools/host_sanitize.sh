@@ -1,0 +1,60 @@
+#!/bin/bash
+# Host-code AddressSanitizer + UndefinedBehaviorSanitizer run of the C ABI and
+# the protocol node.  Device code is NOT instrumented (GPU sanitizers are not
+# available on this pool): -fsanitize goes behind -Xarch_host for the HIP
+# library, and the consumers are built with clang so one sanitizer runtime
+# (clang's, linked statically into each executable) serves the library too.
+#
+#   tools/host_sanitize.sh build     # here (CPU): builds into build/san/
+#   tools/host_sanitize.sh run       # on the GPU box: runs the consumers
+set -eu
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+O="$R/build/san"
+CLANG=/opt/rocm/llvm/bin/clang
+CLANGXX=/opt/rocm/llvm/bin/clang++
+SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer"
+MPI_INC=/opt/conda/include
+MPI_LIB=/opt/conda/lib
+
+case "${1:-}" in
+build)
+  mkdir -p "$O"
+  C="$R/mpi_blockchain_amd/csrc"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -fPIC -shared -std=c++17 -mcode-object-version=5 \
+    -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+    -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer \
+    -I "$R/include" -I "$C" \
+    "$C/pow_api.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" "$C/valu_peak.hip" \
+    -o "$O/libpow_gpu.so"
+  $CLANG -std=c11 -O1 -g $SAN -I "$R/include" "$R/examples/mine_chain.c" \
+    -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/mine_chain"
+  $CLANGXX -std=c++17 -O1 -g $SAN -pthread -I "$R/include" -I "$MPI_INC" \
+    "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' \
+    "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$O/pow_node"
+  echo "built $O"
+  ;;
+run)
+  # Leaks inside the HIP runtime are not ours to judge; everything else aborts.
+  export ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:halt_on_error=1
+  export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
+  export LD_LIBRARY_PATH="$O${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}"
+  "$O/mine_chain" 10 12
+  W=$(mktemp -d)
+  cd "$W"
+  export LD_LIBRARY_PATH="/lib/x86_64-linux-gnu:$MPI_LIB:$LD_LIBRARY_PATH"
+  # d = 9, 4 ranks; then d = 5, 6 ranks with the test pauses so forks, chain
+  # migration and chain service run.  --serial-init 1: every rank finishes its
+  # (sanitizer-slowed) GPU set-up before MPI_Init, so all of them take part.
+  /opt/conda/bin/mpiexec -np 4 "$O/pow_node" --difficulty 9 --serial-init 1
+  echo "chains d=9:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
+  rm -f ./*.out
+  /opt/conda/bin/mpiexec -np 6 "$O/pow_node" --difficulty 5 --serial-init 1 --winner-pause-us 400 --pause-us 200 \
+    > net_d5.log
+  cat net_d5.log
+  echo "chains d=5:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
+  echo "protocol paths taken (lost races, branch conflicts, chain requests):"
+  grep -c "Perdí la carrera\|Conflicto\|TAG_CHAIN_HASH" net_d5.log || true
+  ;;
+*)
+  echo "usage: $0 build|run" >&2; exit 2;;
+esac
