@@ -7,6 +7,7 @@
 #
 #   tools/host_sanitize.sh build     # here (CPU): builds into build/san/
 #   tools/host_sanitize.sh run       # on the GPU box: runs the consumers
+#   tools/host_sanitize.sh tsan-build / tsan-run   # ThreadSanitizer on pow_node
 set -eu
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/build/san"
@@ -55,6 +56,32 @@ run)
   echo "protocol paths taken (lost races, branch conflicts, chain requests):"
   grep -c "Perdí la carrera\|Conflicto\|TAG_CHAIN_HASH" net_d5.log || true
   ;;
+tsan-build)
+  # ThreadSanitizer on pow_node's own code (receive thread, miner thread, GPU
+  # set-up thread); the library and the runtimes below it are not instrumented.
+  mkdir -p "$O"
+  $CLANGXX -std=c++17 -O1 -g -fsanitize=thread -pthread -I "$R/include" -I "$MPI_INC" \
+    "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$R/mpi_blockchain_amd" -lpow_gpu \
+    -Wl,-rpath,"$R/mpi_blockchain_amd" "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$O/pow_node_tsan"
+  echo "built $O/pow_node_tsan"
+  ;;
+tsan-run)
+  S="$O/tsan.supp"
+  printf '%s\n' "called_from_lib:libamdhip64.so" "called_from_lib:libhsa-runtime64.so" \
+    "called_from_lib:libmpi.so" "called_from_lib:libpow_gpu.so" > "$S"
+  export TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1:suppressions=$S"
+  export LD_LIBRARY_PATH="/lib/x86_64-linux-gnu:$MPI_LIB${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}"
+  W=$(mktemp -d)
+  cd "$W"
+  /opt/conda/bin/mpiexec -np 4 "$O/pow_node_tsan" --difficulty 9
+  echo "chains d=9:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
+  rm -f ./*.out
+  /opt/conda/bin/mpiexec -np 6 "$O/pow_node_tsan" --difficulty 5 --winner-pause-us 400 --pause-us 200 > net_d5.log
+  cat net_d5.log
+  echo "chains d=5:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
+  echo "protocol paths taken (lost races, branch conflicts, chain requests):"
+  grep -c "Perdí la carrera\|Conflicto\|TAG_CHAIN_HASH" net_d5.log || true
+  ;;
 *)
-  echo "usage: $0 build|run" >&2; exit 2;;
+  echo "usage: $0 build|run|tsan-build|tsan-run" >&2; exit 2;;
 esac
