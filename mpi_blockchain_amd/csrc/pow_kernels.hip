@@ -125,7 +125,7 @@ __device__ __forceinline__ bool epoch_moved(uint32_t watch, const unsigned int* 
   if (!watch) return false;
   if (blockIdx.x == 0 && threadIdx.x < 64u) {
     const unsigned int now = __hip_atomic_load(host_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (__builtin_amdgcn_readfirstlane(now) != launch_epoch) {
+    if ((uint32_t)__builtin_amdgcn_readfirstlane(now) != launch_epoch) {
       if (threadIdx.x == 0) __hip_atomic_store(cancelled, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return true;
     }
@@ -432,9 +432,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
       uint32_t x = rel, carry = 0;
 #pragma unroll
       for (int i = 8; i >= 0; --i) {
-        uint32_t qq = x / 62u;
-        uint32_t sm = L.base_digit[i] + (x - qq * 62u) + carry;
-        x = qq;
+        uint32_t quo = x / 62u;
+        uint32_t sm = L.base_digit[i] + (x - quo * 62u) + carry;
+        x = quo;
         carry = sm >= 62u ? 1u : 0u;
         dg[i] = carry ? sm - 62u : sm;
       }
