@@ -1,0 +1,65 @@
+"""Protocol soak: many short forking networks of pow_node ranks on one GPU.
+
+Each run is an mpiexec of N GPU ranks at a low difficulty with the fork knobs
+of tests/test_node_gpu.py (--winner-pause-us, --pause-us), so lost races,
+branch conflicts and chain migrations fire in every run.  A run passes when
+mpiexec exits 0 within its time limit, no rank rejects a block as invalid
+("Error duro"), and every chain dump a rank wrote is consistent (linked,
+consecutive, solving) with at least one complete 10-block chain.
+
+The loop stops at the first failed run (no retries): its output is printed.
+
+    python tools/protocol_soak.py --runs 40 --ranks 8 --difficulty 5
+"""
+import argparse
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from mpi_blockchain_amd.node import run_network  # noqa: E402
+from test_node_gpu import FORK_MSGS, check_chain  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runs", type=int, default=40)
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--difficulty", type=int, default=5)
+    ap.add_argument("--timeout", type=float, default=60)
+    a = ap.parse_args()
+    extra = ("--winner-pause-us", "400", "--pause-us", "200")
+    walls, forks = [], 0
+    for i in range(a.runs):
+        with tempfile.TemporaryDirectory() as wd:
+            t0 = time.perf_counter()
+            run = run_network(a.ranks, wd, difficulty=a.difficulty, blocks=10, timeout=a.timeout, extra_args=extra)
+            wall = time.perf_counter() - t0
+        ok = run.returncode == 0 and "Error duro" not in run.stdout
+        complete = 0
+        if ok:
+            try:
+                complete = sum(check_chain(e, 10, a.difficulty) for e in run.chains.values())
+            except AssertionError:
+                ok = False
+        ok = ok and complete > 0
+        n_fork = sum(run.stdout.count(m) for m in FORK_MSGS)
+        forks += n_fork
+        walls.append(wall)
+        print(f"run {i + 1}/{a.runs}: rc {run.returncode} wall {wall:.2f} s, dumps {len(run.chains)}, "
+              f"complete {complete}, fork-path lines {n_fork} -> {'ok' if ok else 'FAIL'}", flush=True)
+        if not ok:
+            print(run.stdout[-6000:])
+            return 1
+    walls.sort()
+    print(f"{a.runs} networks of {a.ranks} ranks at d = {a.difficulty}: all passed; "
+          f"wall median {walls[len(walls) // 2]:.2f} s, max {walls[-1]:.2f} s; {forks} fork-path lines in total")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
