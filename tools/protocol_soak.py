@@ -10,9 +10,15 @@ consecutive, solving) with at least one complete 10-block chain.
 The loop stops at the first failed run (no retries): its output is printed.
 
     python tools/protocol_soak.py --runs 40 --ranks 8 --difficulty 5
+    python tools/protocol_soak.py --runs 20 --ranks 2 --ref 2 --difficulty 9   # mixed networks
+
+With --ref K the job also holds K ranks of the REFERENCE's own binary
+(oracle/_ref/blockchain_ref, whose difficulty is its macro, 9), as in
+tests/test_node_gpu.py::test_mixed_with_reference_nodes.
 """
 import argparse
 import os
+import re
 import sys
 import tempfile
 import time
@@ -31,13 +37,20 @@ def main() -> int:
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--difficulty", type=int, default=5)
     ap.add_argument("--timeout", type=float, default=60)
+    ap.add_argument("--ref", type=int, default=0, help="reference (CPU) ranks in the same job")
     a = ap.parse_args()
     extra = ("--winner-pause-us", "400", "--pause-us", "200")
+    ref = dict(ref_binary=os.path.join(ROOT, "oracle", "_ref", "blockchain_ref"), n_ref=a.ref) if a.ref else {}
+    if a.ref:
+        if a.difficulty != 9:
+            ap.error("the reference binary mines at its DEFAULT_DIFFICULTY macro, 9")
+        extra = ("--pause-ms", "5")  # as the mixed test: GPU ranks leave the reference ranks room to win
     walls, forks = [], 0
     for i in range(a.runs):
         with tempfile.TemporaryDirectory() as wd:
             t0 = time.perf_counter()
-            run = run_network(a.ranks, wd, difficulty=a.difficulty, blocks=10, timeout=a.timeout, extra_args=extra)
+            run = run_network(a.ranks, wd, difficulty=a.difficulty, blocks=10, timeout=a.timeout, extra_args=extra,
+                              **ref)
             wall = time.perf_counter() - t0
         ok = run.returncode == 0 and "Error duro" not in run.stdout
         complete = 0
@@ -48,15 +61,21 @@ def main() -> int:
                 ok = False
         ok = ok and complete > 0
         n_fork = sum(run.stdout.count(m) for m in FORK_MSGS)
+        cross = ""
+        if a.ref:  # blocks adopted across implementations (reference ranks are 0..ref-1)
+            acc = [(int(r), int(s_)) for r, s_ in
+                   re.findall(r"\[(\d+)\] Agregado a la lista bloque con index \d+ enviado por (\d+)", run.stdout)]
+            cross = (f", ref<-gpu {sum(r < a.ref <= s_ for r, s_ in acc)}"
+                     f", gpu<-ref {sum(s_ < a.ref <= r for r, s_ in acc)}")
         forks += n_fork
         walls.append(wall)
         print(f"run {i + 1}/{a.runs}: rc {run.returncode} wall {wall:.2f} s, dumps {len(run.chains)}, "
-              f"complete {complete}, fork-path lines {n_fork} -> {'ok' if ok else 'FAIL'}", flush=True)
+              f"complete {complete}, fork-path lines {n_fork}{cross} -> {'ok' if ok else 'FAIL'}", flush=True)
         if not ok:
             print(run.stdout[-6000:])
             return 1
     walls.sort()
-    print(f"{a.runs} networks of {a.ranks} ranks at d = {a.difficulty}: all passed; "
+    print(f"{a.runs} networks of {a.ranks} GPU + {a.ref} reference ranks at d = {a.difficulty}: all passed; "
           f"wall median {walls[len(walls) // 2]:.2f} s, max {walls[-1]:.2f} s; {forks} fork-path lines in total")
     return 0
 
