@@ -137,7 +137,7 @@ class GpuMiner:
         n = ctypes.c_size_t()
         check(self.L.pow_sweep(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), cap, ctypes.byref(n)))
-        return out[: n.value].copy()
+        return out[: n.value]  # a view: copying 33.6 MB (a 2^32 window at d = 9) again costs ~3 ms
 
     def sweep_count(self, tmpl: Block, start: int, count: int, difficulty: int,
                     dev_out=None, cap: int = 0) -> tuple[int, int | None]:
