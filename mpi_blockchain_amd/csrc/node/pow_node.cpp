@@ -29,7 +29,17 @@
 //     receive loop polls with a backoff instead of MPICH's spinning probe
 //     (T12: the reference burns a core per rank there).
 //
-//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US] [--winner-pause-us US]
+// Start line.  The reference's ranks start mining as soon as MPI_Init returns
+// (blockchain.cpp:15 -> node.cpp:396), and MPI_Init synchronises the job.
+// Here GPU set-up (160-220 ms per process) runs beside MPI_Init, so ranks
+// would leave it at different times: an MPI_Barrier after both puts them back
+// on one start line before any miner starts.  In a job that mixes in
+// reference ranks (which never join a barrier) pass --serial-init 1: GPU
+// set-up then runs BEFORE MPI_Init, and MPI_Init is the start line, as in the
+// reference.
+//
+//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US]
+//            [--winner-pause-us US] [--serial-init 0|1] [--hold-first 0|1]
 #include <mpi.h>
 #include <unistd.h>
 
@@ -72,6 +82,9 @@ struct Options {
   unsigned pause_us = 0;    // sleep a random 0..pause_us us before each round (tests: lets slower
                             // CPU ranks compete, and decorrelates GPU ranks so forks happen)
   bool serial_init = false; // --serial-init 1: GPU set-up before MPI_Init instead of beside it
+                            // (and no start barrier: mixed jobs with reference ranks)
+  bool hold_first = false;  // tests: every rank mines block 1, then all publish it after one
+                            // MPI_Barrier, so every rank receives a rival block 1 (a certain fork)
 };
 
 // MPI_Probe that sleeps between polls instead of spinning.  MPICH's blocking
@@ -91,8 +104,11 @@ void probe_any(MPI_Status* st) {
   }
 }
 
-std::string hash_of(const pow_block& b) { return std::string(b.block_hash); }
-std::string prev_of(const pow_block& b) { return std::string(b.previous_block_hash); }
+// Bounded: a peer's block need not hold a NUL inside its 256-byte fields.
+std::string hash_of(const pow_block& b) { return std::string(b.block_hash, strnlen(b.block_hash, POW_HASH_SIZE)); }
+std::string prev_of(const pow_block& b) {
+  return std::string(b.previous_block_hash, strnlen(b.previous_block_hash, POW_HASH_SIZE));
+}
 
 class Node {
  public:
@@ -352,7 +368,28 @@ class Node {
         fprintf(stderr, "[%d] pow_mine_any: %s\n", rank_, pow_last_error());
         MPI_Abort(MPI_COMM_WORLD, 1);
       }
-      if (rc == 1) {  // node.cpp:311-327
+      if (rc == 1 && opt_.hold_first && solved.index == 1) {
+        // --hold-first: adopt block 1, wait until every rank has mined its
+        // own block 1, then publish.  Each rank then receives rival blocks 1
+        // while its chain is at index 1: "Conflicto de branch" (node.cpp:235)
+        // on every rank, deterministically.
+        bool adopted = false;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          if (last_->index < solved.index) {
+            const std::string h = hash_of(solved);
+            blocks_.insert({h, solved});
+            set_last(&blocks_.at(h));
+            printf("[%d] Agregué un producido con index %u \n", rank_, last_->index);
+            adopted = true;
+          }
+        }
+        MPI_Barrier(MPI_COMM_WORLD);  // nobody sends before this, so our block 1 stands
+        if (adopted) {
+          std::lock_guard<std::mutex> g(mu_);
+          send_block_to_everyone(blocks_.at(hash_of(solved)));
+        }
+      } else if (rc == 1) {  // node.cpp:311-327
         std::lock_guard<std::mutex> g(mu_);
         if (last_->index < solved.index) {
           const std::string h = hash_of(solved);
@@ -373,7 +410,8 @@ class Node {
 // GPU set-up (HIP start-up, 160-220 ms per process, two contexts, kernel
 // warm-up) runs on a thread beside MPI_Init, which itself waits for every
 // process of the job, so a rank's start-up costs the longer of the two rather
-// than their sum.  The miner starts only once both are done.  (--serial-init 1
+// than their sum.  The miner starts only once both are done and every rank
+// has passed the start barrier in main().  (--serial-init 1
 // runs it before MPI_Init instead: then no reference rank of a mixed job can
 // start mining while a GPU rank is still initialising.)  The device is the
 // node-local rank (from the launcher's environment) modulo the visible GPUs.
@@ -457,6 +495,7 @@ int main(int argc, char** argv) {
     else if (k == "--pause-us") o.pause_us = (unsigned)v;
     else if (k == "--winner-pause-us") o.winner_pause_us = (unsigned)v;
     else if (k == "--serial-init") o.serial_init = v != 0;
+    else if (k == "--hold-first") o.hold_first = v != 0;
   }
   Node n(o);
   int gpu_rc = 0;
@@ -480,6 +519,9 @@ int main(int argc, char** argv) {
   }
   setbuf(stdout, nullptr);  // blockchain.cpp:27-28
   setbuf(stderr, nullptr);
+  // One start line for every rank (see the header): GPU set-up ended at a
+  // different time on each rank.  With --serial-init, MPI_Init was it.
+  if (!o.serial_init) MPI_Barrier(MPI_COMM_WORLD);
   n.run();
   MPI_Finalize();
   return 0;

@@ -371,6 +371,12 @@ void digest_out(const uint32_t* h, uint8_t* digest, char* hex) {
 
 }  // namespace
 
+// The caller's cancel word is written by another thread (the receive loop):
+// read it with an acquire load, not a plain volatile read.
+bool cancel_moved(const volatile uint32_t* cancel_word, uint32_t epoch) {
+  return cancel_word && __atomic_load_n(const_cast<const uint32_t*>(cancel_word), __ATOMIC_ACQUIRE) != epoch;
+}
+
 int pow_ctx_device(const pow_ctx* ctx) { return ctx->device; }
 void* pow_ctx_stream(const pow_ctx* ctx) { return (void*)ctx->stream; }
 int pow_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
@@ -608,7 +614,7 @@ int pow_sweep_device(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   if (int rc = run_search(ctx, ctr_start, ctr_count, diff_bits, 0, dev_out, cap32)) return rc;
   // The kernel writes 32-entry blocks to dev_out and each wave's last < 32
   // solutions to ctx->d_tail: append those behind the blocks.
-  const uint64_t nblk = ctx->h_res->count, ntail = ctx->h_res->tail;
+  const uint64_t nblk = ctx->h_res->count, ntail = ctx->h_res->tail;  // count is 64-bit: d = 0 fills 2^32
   if (ntail > ctx->tail_cap) return fail(POW_EHIP, "sweep tail overflow (%llu)", (unsigned long long)ntail);
   if (ntail && nblk < cap32) {
     const uint64_t k = std::min<uint64_t>(ntail, cap32 - nblk);
@@ -626,7 +632,8 @@ int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t 
   if (!ctx || !n_found) return fail(POW_EINVAL, "null");
   if (cap && !out_ctrs) return fail(POW_EINVAL, "cap without buffer");
   if (int rc = set_dev(ctx)) return rc;
-  if (cap > 0xFFFFFFFFu) cap = 0xFFFFFFFFu;
+  // The device radix sort takes a signed 32-bit item count (hipCUB).
+  if (cap > 0x7FFFFFFFu) return fail(POW_EINVAL, "cap %zu > 2^31-1 (the host-list form sorts on the device)", cap);
   if (cap > ctx->out_cap) {
     (void)hipFree(ctx->d_out);
     (void)hipFree(ctx->d_alt);
@@ -697,7 +704,7 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   uint64_t done = 0;
   bool first = true;
   while (done < ctr_count) {
-    if (cancel_word && *cancel_word != epoch) break;
+    if (cancel_moved(cancel_word, epoch)) break;
     const bool lat = first && use_lat;
     const uint64_t cap = lat ? ctx->lat_max : (uint64_t)1 << 30;
     const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(step, cap), ctr_count - done);
@@ -709,7 +716,7 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
     done += n;
     // cancelled while the launch ran (pow_cancel stops it early; its result,
     // if any, belongs to a stale template and, in lowest mode, may not be final)
-    if ((cancel_word && *cancel_word != epoch) || ctx->h_res->cancelled) break;
+    if (cancel_moved(cancel_word, epoch) || ctx->h_res->cancelled) break;
     if (ctx->h_res->min_rel != ~0ull) {
       const PowResult& r = *ctx->h_res;
       // The latency kernel records its first POW_HITS hits with their digests.

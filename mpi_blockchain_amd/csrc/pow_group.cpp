@@ -222,7 +222,7 @@ int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint
         snprintf(local_err, sizeof local_err, "%s", pow_last_error());
       }
     }
-    if (cancel_word && *cancel_word != epoch) v[1] = 0;
+    if (cancel_moved(cancel_word, epoch)) v[1] = 0;
     if (int rc = group_allreduce(g, v, 3, ncclMin)) return rc;
     if (hashes_done) *hashes_done = hashes;
     if (v[2] == 0)  // every rank leaves the search together

@@ -82,19 +82,20 @@ __device__ __forceinline__ void const_chunk(St& t, cptr kwbase, uint32_t dep) {
 __device__ __forceinline__ void flush_stage(uint32_t* wst, uint32_t& nst, uint32_t lane, PowResult* res,
                                             uint32_t* out, uint32_t cap) {
   const uint32_t n = nst & ~31u;
-  uint32_t got = 0;
-  if (lane == 0) got = atomicAdd(&res->count, n);
-  const uint32_t base = __builtin_amdgcn_readfirstlane(got);
+  unsigned long long got = 0;
+  if (lane == 0) got = atomicAdd(&res->count, (unsigned long long)n);
+  const unsigned long long base = uniform64(got);  // 64-bit: 2^32 solutions at d = 0
   const uint32_t i = lane * 4u;  // n <= 96: one pass of <= 24 lanes
   if (i < n) {
     const uint32_t e0 = wst[i], e1 = wst[i + 1u], e2 = wst[i + 2u], e3 = wst[i + 3u];
-    if (base + i + 4u <= cap && ((uintptr_t)out & 15u) == 0) {
-      *reinterpret_cast<uint4*>(out + base + i) = make_uint4(e0, e1, e2, e3);
+    const unsigned long long o = base + i;
+    if (o + 4u <= cap && ((uintptr_t)out & 15u) == 0) {
+      *reinterpret_cast<uint4*>(out + o) = make_uint4(e0, e1, e2, e3);
     } else {
-      if (base + i < cap) out[base + i] = e0;
-      if (base + i + 1u < cap) out[base + i + 1u] = e1;
-      if (base + i + 2u < cap) out[base + i + 2u] = e2;
-      if (base + i + 3u < cap) out[base + i + 3u] = e3;
+      if (o < cap) out[o] = e0;
+      if (o + 1u < cap) out[o + 1u] = e1;
+      if (o + 2u < cap) out[o + 2u] = e2;
+      if (o + 3u < cap) out[o + 3u] = e3;
     }
   }
   const uint32_t rem = nst - n;  // source [n, n + rem) and target [0, rem) do not overlap (n >= 32 > rem)

@@ -93,8 +93,10 @@ struct PowHit {
 struct PowResult {
   unsigned long long min_rel;  // lowest solving (counter - ctr_start); ~0 = none
   unsigned long long hashes;   // mine mode: trials actually computed
-  unsigned int count;          // sweep: solutions in the main list (32-entry blocks)
+  unsigned long long count;    // sweep: solutions in the main list (32-entry blocks); 64-bit, since
+                               // at d = 0 a 2^32 window has 2^32 solutions
   unsigned int next;           // next prefix chunk to hand out (dynamic work queue)
+  unsigned int pad0;
   unsigned int tail;           // sweep: solutions in tail_buf (< 32 per wave)
   unsigned int tail_cap;       // entries of tail_buf
   unsigned int* tail_buf;      // sweep: each wave's last < 32 solutions (appended by the host);
@@ -126,5 +128,7 @@ int pow_ctx_device(const struct pow_ctx* ctx);
 void* pow_ctx_stream(const struct pow_ctx* ctx);  // the ctx's hipStream_t
 // Record `msg` for pow_last_error(); returns `code`.
 int pow_set_error(int code, const char* msg);
+// True once another thread moved the caller's cancel word off `epoch` (acquire load).
+bool cancel_moved(const volatile uint32_t* cancel_word, uint32_t epoch);
 }
 #endif

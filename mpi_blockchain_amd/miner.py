@@ -131,8 +131,8 @@ class GpuMiner:
 
     def sweep(self, tmpl: Block, start: int, count: int, difficulty: int, cap: int | None = None) -> np.ndarray:
         """Ascending (counter - start) of every solving counter (count <= 2^32)."""
-        if cap is None:
-            cap = int(min(count, (count >> min(difficulty, 63)) * 2 + 4096))
+        if cap is None:  # pow_sweep sorts on the device: at most 2^31 - 1 entries
+            cap = int(min(count, (count >> min(difficulty, 63)) * 2 + 4096, (1 << 31) - 1))
         out = np.zeros(max(cap, 1), dtype=np.uint32)
         n = ctypes.c_size_t()
         check(self.L.pow_sweep(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
