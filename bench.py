@@ -41,36 +41,80 @@ def s0_block():
     return make_block(1, 0, 9, 1700000000, b"")
 
 
-def cpu_baseline(seconds: float = 1.5) -> dict | None:
-    """Reference loop (oracle/_ref, compiled from /root/reference's own
-    block.cpp + picosha2.h) on the host cores; falls back to the C
-    restatement (oracle/liboracle.so) if the reference build is absent."""
+def host_cpu_info() -> dict:
+    """Host CPUs this process may use: affinity mask, cgroup CPU quota
+    (cgroup v2 cpu.max), and lscpu's topology."""
+    info = {"os_cpu_count": os.cpu_count()}
     try:
-        cores = len(os.sched_getaffinity(0))
+        info["affinity"] = len(os.sched_getaffinity(0))
     except Exception:
-        cores = os.cpu_count() or 1
-    procs = max(1, min(16, cores))
-    out = {}
+        info["affinity"] = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        info["cgroup_cpu_quota"] = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        keys = {"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "CPU(s)": "cpus"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keys:
+                info[keys[k.strip()]] = v.strip()
+    except Exception:
+        pass
+    return info
+
+
+def cpu_baseline(seconds: float = 1.5) -> dict | None:
+    """The reference's mining loop body (oracle/_ref, compiled from
+    /root/reference's own block.cpp + picosha2.h) on ALL host CPUs this job
+    may use: one MPI rank per CPU of the affinity mask, launched with
+    mpiexec as the reference is (Makefile:24), -O2 and -O0 (as shipped).
+    Falls back to one forked process per CPU without MPI, and to the C
+    restatement (oracle/liboracle.so) without the reference build."""
+    host = host_cpu_info()
+    ranks = max(1, host["affinity"])
+    quota = host.get("cgroup_cpu_quota")
+    usable = min(ranks, quota) if quota else ranks  # CPUs' worth of time the job can get
+    out, how = {}, None
+    try:
+        from mpi_blockchain_amd.build import mpi_available
+        from mpi_blockchain_amd.node import MPIEXEC, mpi_env
+        use_mpi = mpi_available()
+    except Exception:
+        use_mpi = False
     for flav in ("O2", "O0"):
+        mpi_exe = os.path.join(ROOT, "oracle", "_ref", f"ref_cpu_bench_mpi_{flav}")
         exe = os.path.join(ROOT, "oracle", "_ref", f"ref_cpu_bench_{flav}")
-        if os.path.exists(exe):
-            try:
-                r = subprocess.run([exe, str(procs), str(seconds)], capture_output=True, text=True,
-                                   timeout=120, check=True)
-                out[flav] = json.loads(r.stdout.strip().splitlines()[-1])
-            except Exception as e:  # pragma: no cover
-                out[flav] = {"error": str(e)}
+        try:
+            if use_mpi and os.path.exists(mpi_exe):
+                cmd, how = ["timeout", "-k", "10", "180", MPIEXEC, "-np", str(ranks), mpi_exe, str(seconds)], "mpi"
+                r = subprocess.run(cmd, capture_output=True, text=True, check=True, env=mpi_env(), cwd="/tmp")
+            elif os.path.exists(exe):
+                cmd, how = [exe, str(ranks), str(seconds)], "fork"
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, check=True)
+            else:
+                continue
+            out[flav] = json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as e:  # pragma: no cover
+            out[flav] = {"error": str(e)[-300:]}
     if "O2" in out and "trials_per_s" in out["O2"]:
         o2 = out["O2"]
-        res = {"value": round(o2["trials_per_s"], 1), "unit": "trials/s", "cores": procs, "kind": "reference",
+        launch = (f"mpiexec -np {ranks} (one MPI rank per CPU)" if how == "mpi"
+                  else f"{ranks} forked processes (one per CPU)")
+        res = {"value": round(o2["trials_per_s"], 1), "unit": "trials/s", "cores": ranks, "kind": "reference",
                "sample": (f"reference proof_of_work loop body (node.cpp:292-308; /root/reference block.cpp + "
-                          f"picosha2.h built -O2 by oracle/Makefile), {procs} processes x {seconds} s, "
-                          f"rand() nonces, difficulty 9")}
-        res["per_core"] = round(o2["trials_per_s"] / procs, 1)
+                          f"picosha2.h built -O2 by oracle/Makefile), {launch} x {seconds} s, rand() nonces, "
+                          f"difficulty 9")}
+        res["per_core"] = round(o2["trials_per_s"] / ranks, 1)
+        # With a CPU quota below the affinity mask the ranks share `usable` CPUs' worth of time.
+        res["per_usable_cpu"] = round(o2["trials_per_s"] / usable, 1)
         if "O0" in out and "trials_per_s" in out["O0"]:
             res["as_shipped_O0"] = round(out["O0"]["trials_per_s"], 1)
-            res["as_shipped_O0_per_core"] = round(out["O0"]["trials_per_s"] / procs, 1)
-        res["host_cpus"] = {"nproc": os.cpu_count(), "affinity": cores, "used": procs}
+            res["as_shipped_O0_per_usable_cpu"] = round(out["O0"]["trials_per_s"] / usable, 1)
+        res["host_cpus"] = dict(host, ranks=ranks, usable=usable)
         return res
     # restatement fallback ("port")
     try:
@@ -78,6 +122,7 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
 
         from oracle.oracle import Oracle, make_oblock
 
+        procs = int(max(1, min(ranks, usable)))
         O = Oracle()
         b = make_oblock(1, 0, 9, 1700000000, b"")
         n = 1 << 18
@@ -85,7 +130,8 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
         O.L.oracle_sweep(ctypes.byref(b), 0, n * procs, 9, None, 0, procs)
         dt = time.perf_counter() - t
         return {"value": round(n * procs / dt, 1), "unit": "trials/s", "cores": procs, "kind": "port",
-                "sample": f"C restatement (oracle/pow_oracle.c) sweep of {n * procs} counters on {procs} threads"}
+                "sample": f"C restatement (oracle/pow_oracle.c) sweep of {n * procs} counters on {procs} threads",
+                "host_cpus": host}
     except Exception as e:  # pragma: no cover
         return {"error": str(e)}
 

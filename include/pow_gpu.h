@@ -173,6 +173,46 @@ int pow_dev_free(pow_ctx* ctx, void* p);
 /* Copy `bytes` from a device pointer to host memory (synchronous). */
 int pow_dev_read(pow_ctx* ctx, const void* dev, void* host, size_t bytes);
 
+/* ---- cross-GPU stop board (one node) ------------------------------------ */
+/* The reference's ranks hear of a rival's block only through MPI, between
+ * trials (node.cpp:315, 404).  When several GPUs search ONE template together
+ * (pow_group_*, BASELINE config 4), the finder must stop the others inside
+ * their running launches: a collective only runs between kernels.  A board is
+ * a page of host memory every GPU of the node maps, one 64-bit slot per rank.
+ * A context bound to slot s of a board, for the search tagged `tag`:
+ *   - stores every hit of its pow_mine / pow_mine_any launches into slot s,
+ *     from the kernel itself (system-scope store over PCIe);
+ *   - stops, within one inner step, as soon as another slot holds a solution
+ *     of the same tag that makes its remaining counters moot: in
+ *     pow_mine_any any peer solution; in pow_mine a peer solution below the
+ *     counters it would still compute (the lowest-counter result stays exact:
+ *     counters below the peer's are always finished).
+ * Such a call then returns 0 (the peer's result wins the caller's
+ * reduction).  pow_group_* use a board automatically; these entry points are
+ * for callers that drive several contexts themselves. */
+#define POW_BOARD_MAX_SLOTS 64
+#define POW_BOARD_MAX_TAG 1023
+typedef struct pow_board pow_board;
+/* name NULL: memory private to this process (contexts of one process, one
+ * host thread per GPU).  name "/x": POSIX shared memory shared by every
+ * process of the node that opens the same name (one process per GPU); it is
+ * created zeroed if absent.  nslots 1..64.  Opening, posting and peeking
+ * need no GPU; the first pow_board_bind maps the page for the GPUs. */
+int pow_board_open(const char* name, int nslots, pow_board** out);
+/* Remove a named board's name (processes that opened it keep their mapping). */
+int pow_board_unlink(const char* name);
+/* Unbind every context from the board first. */
+void pow_board_close(pow_board* b);
+/* Bind ctx to `slot` for the search tagged `tag` (1..1023; use a new tag per
+ * search so stale slots are ignored) and mark the slot "nothing found yet";
+ * b = NULL unbinds.  The ctx's launches watch and feed the board until
+ * unbound. */
+int pow_board_bind(pow_ctx* ctx, pow_board* b, int slot, uint32_t tag);
+/* Host-side view: publish `ctr` in `slot` for `tag`; lowest counter any other
+ * slot holds for `tag` (UINT64_MAX = none). */
+int pow_board_post(pow_board* b, int slot, uint32_t tag, uint64_t ctr);
+int pow_board_peek(const pow_board* b, int except_slot, uint32_t tag, uint64_t* min_ctr);
+
 /* ---- sharded search over several GPUs (RCCL) --------------------------- */
 /* One template mined cooperatively by `nranks` GPUs, one pow_ctx each (one
  * process or host thread per GPU).  The reference has no such mode: its ranks
@@ -196,7 +236,10 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
 void pow_group_destroy(pow_group* g);
 /* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream. */
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);
-/* pow_mine over all ranks: rounds of `round_size` counters (0 = adaptive:
+/* On one node the ranks also share a stop board (named after the id, opened
+ * by pow_group_init): a rank's hit stops the other GPUs inside their running
+ * launches, not only at the round's all-reduce.
+ * pow_mine over all ranks: rounds of `round_size` counters (0 = adaptive:
  * ~4x the expected trials first, then 4x larger up to 2^30 per rank), each
  * split into static shards; each rank mines the lowest solving
  * counter of its shard, then one 24-byte ncclAllReduce(ncclMin) per round
@@ -207,6 +250,15 @@ int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);
 int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
                    uint64_t round_size, unsigned diff_bits, const volatile uint32_t* cancel_word,
                    uint32_t epoch, pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
+/* pow_mine_any over all ranks (time-to-block: the first solution any GPU
+ * finds ends the search on every GPU).  Rounds of `round_size` counters (0 =
+ * 2^32 per rank), static shards; the first hit stops the node's other GPUs
+ * through the board, and one 24-byte all-reduce(min) per round agrees on the
+ * winner: the lowest counter among the solutions the ranks found.  Same
+ * outputs and return codes as pow_group_mine, the same result on every rank. */
+int pow_group_mine_any(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                       uint64_t round_size, unsigned diff_bits, const volatile uint32_t* cancel_word,
+                       uint32_t epoch, pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,7 @@ POW_OK, POW_EINVAL, POW_ENOSPC, POW_EHIP, POW_ENODEV, POW_ECOMM = 0, -1, -2, -3,
 _ERRNAMES = {POW_EINVAL: "POW_EINVAL", POW_ENOSPC: "POW_ENOSPC", POW_EHIP: "POW_EHIP",
              POW_ENODEV: "POW_ENODEV", POW_ECOMM: "POW_ECOMM"}
 GROUP_ID_BYTES = 128
+BOARD_MAX_SLOTS, BOARD_MAX_TAG = 64, 1023
 POW_REDUCE_MIN, POW_REDUCE_MAX, POW_REDUCE_SUM = 0, 1, 2
 
 
@@ -109,6 +110,14 @@ def load() -> ctypes.CDLL:
         "pow_group_allreduce_u64": ([ctypes.c_void_p, c_u64p, ctypes.c_size_t, ctypes.c_int], ctypes.c_int),
         "pow_group_mine": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
                             ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
+        "pow_group_mine_any": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                                ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
+        "pow_board_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "pow_board_unlink": ([ctypes.c_char_p], ctypes.c_int),
+        "pow_board_close": ([ctypes.c_void_p], None),
+        "pow_board_bind": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32], ctypes.c_int),
+        "pow_board_post": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64], ctypes.c_int),
+        "pow_board_peek": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, c_u64p], ctypes.c_int),
         "pow_valu_peak": ([ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
                           ctypes.c_int),
     }
@@ -124,7 +133,9 @@ EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_las
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
-           "pow_group_destroy", "pow_group_allreduce_u64", "pow_group_mine")
+           "pow_group_destroy", "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",
+           "pow_board_open", "pow_board_unlink", "pow_board_close", "pow_board_bind", "pow_board_post",
+           "pow_board_peek")
 
 
 def check(rc: int) -> int:

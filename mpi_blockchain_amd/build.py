@@ -17,7 +17,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libpow_gpu.so")
-SOURCES = ["pow_api.cpp", "pow_group.cpp", "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip"]
+SOURCES = ["pow_api.cpp", "pow_board.cpp", "pow_group.cpp", "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip"]
 HEADERS = ["pow_template.h", "sha256_dev.h"]
 INCLUDES = [os.path.join(ROOT, "include", h) for h in ("pow_gpu.h", "pow_tools.h")]
 ARCH = "gfx950"

@@ -177,6 +177,11 @@ struct pow_ctx {
   std::atomic<bool> armed{false};       // pow_cancel has published an epoch
   uint32_t launch_epoch = 0;            // mine calls: the caller's epoch ...
   bool watch_epoch = false;             // ... watched on the GPU when armed
+  pow_board* board = nullptr;           // bound stop board (pow_board_bind) ...
+  const unsigned long long* board_dev = nullptr;  // ... its slots, device address
+  int board_slot = -1;
+  uint32_t board_tag = 0;
+  bool board_off = false;               // winner re-hash: not part of the search
   PowConsts* d_consts = nullptr;  // = &d_blob->consts
   PowResult* d_res = nullptr;     // = &d_blob->res
   PowResult* h_res = nullptr;  // pinned read-back of d_res
@@ -198,8 +203,31 @@ struct pow_ctx {
 
 namespace {
 
-int stage_result(pow_ctx* ctx, bool with_tail);
+int stage_result(pow_ctx* ctx, bool with_tail, uint64_t abs_start);
 void digest_out(const uint32_t* h, uint8_t* digest, char* hex);
+
+// What a mine launch watches: the caller's epoch (pow_cancel) and the bound
+// stop board.  abs_start = absolute counter of the launch's relative 0.
+void fill_watch(const pow_ctx* ctx, PowWatch& w, uint64_t abs_start) {
+  memset(&w, 0, sizeof w);
+  w.watch_epoch = ctx->watch_epoch && ctx->armed.load(std::memory_order_acquire) ? 1u : 0u;
+  w.host_epoch = ctx->d_epoch;
+  w.launch_epoch = ctx->launch_epoch;
+  w.abs_start = abs_start;
+  if (ctx->board && !ctx->board_off) {
+    w.board = ctx->board_dev;
+    w.board_mine = const_cast<unsigned long long*>(ctx->board_dev) + ctx->board_slot;
+    w.board_n = (uint32_t)pow_board_nslots(ctx->board);
+    w.board_tag = ctx->board_tag;
+  }
+}
+
+// Lowest counter a peer published for the bound search (host view).
+uint64_t board_peer_min(const pow_ctx* ctx) {
+  uint64_t m = UINT64_MAX;
+  if (ctx->board && !ctx->board_off) pow_board_peek(ctx->board, ctx->board_slot, ctx->board_tag, &m);
+  return m;
+}
 
 int set_dev(const pow_ctx* ctx) {
   HIP_OK(hipSetDevice(ctx->device));
@@ -249,7 +277,7 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   PowLaunch L;
   int rc = make_launch(start, count, diff, cap, mode, &L);
   if (rc) return rc;
-  if (int rc2 = stage_result(ctx, true)) return rc2;
+  if (int rc2 = stage_result(ctx, true, start)) return rc2;
   const unsigned grid = grid_for(ctx, L.n_prefix);
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_OK(pow_launch_search((int)mode, diff > 32 || ctx->force_full, grid, ctx->stream, ctx->d_consts, L, dev_out,
@@ -291,9 +319,7 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   L.count = count;
   L.diff = diff;
   L.thr = diff >= 32 ? 0u : (0xFFFFFFFFu >> diff);
-  L.watch_epoch = ctx->watch_epoch && ctx->armed.load(std::memory_order_acquire) ? 1u : 0u;
-  L.host_epoch = ctx->d_epoch;
-  L.launch_epoch = ctx->launch_epoch;
+  fill_watch(ctx, L.watch, start);
   // A 256-thread workgroup puts one wave on each SIMD of its CU.
   const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
@@ -331,13 +357,12 @@ int upload_consts(pow_ctx* ctx, const pow_block* tmpl) {
 }
 
 // Reset the device result words (and upload pending constants) before a launch.
-int stage_result(pow_ctx* ctx, bool with_tail) {
+int stage_result(pow_ctx* ctx, bool with_tail, uint64_t abs_start) {
   PowResult& r = ctx->h_blob->res;
   memset(&r, 0, sizeof r);
   r.min_rel = ~0ull;
-  r.launch_epoch = ctx->launch_epoch;
-  r.watch_epoch = ctx->watch_epoch && ctx->armed.load(std::memory_order_acquire) ? 1u : 0u;
-  r.host_epoch = ctx->d_epoch;
+  r.peer_abs = ~0ull;
+  fill_watch(ctx, r.watch, abs_start);
   if (with_tail) {
     r.tail_buf = ctx->d_tail;
     r.tail_cap = ctx->tail_cap;
@@ -378,6 +403,7 @@ bool cancel_moved(const volatile uint32_t* cancel_word, uint32_t epoch) {
 }
 
 int pow_ctx_device(const pow_ctx* ctx) { return ctx->device; }
+void pow_ctx_set_stats(pow_ctx* ctx, const pow_stats& s) { ctx->stats = s; }
 void* pow_ctx_stream(const pow_ctx* ctx) { return (void*)ctx->stream; }
 int pow_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
@@ -435,6 +461,7 @@ int pow_init(int device, pow_ctx** out) {
   if (ctx->d_lat && ctx->h_lat) {
     PowResult init{};
     init.min_rel = ~0ull;
+    init.peer_abs = ~0ull;
     chk(hipMemcpy(ctx->d_lat, &init, sizeof init, hipMemcpyHostToDevice), "hipMemcpy");
     chk(hipHostGetDevicePointer((void**)&ctx->d_lat_host, ctx->h_lat, 0), "hipHostGetDevicePointer");
   }
@@ -701,10 +728,16 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   const unsigned lat_wps = diff_bits <= 17 ? 1 : diff_bits <= 19 ? 2 : 4;
   uint64_t step = use_lat ? std::max<uint64_t>(1ull << 12, 1ull << (dcap + 4))
                           : (any ? 1ull << 30 : std::max<uint64_t>(1ull << 12, 1ull << std::min(dcap + 2, 30u)));
+  // Bound stop board: a peer's solution makes the rest of the range moot —
+  // any peer solution in any-mode, one below `next` in lowest mode.
+  auto preempted = [&](uint64_t next) {
+    const uint64_t m = board_peer_min(ctx);
+    return any ? m != UINT64_MAX : m < next;
+  };
   uint64_t done = 0;
   bool first = true;
   while (done < ctr_count) {
-    if (cancel_moved(cancel_word, epoch)) break;
+    if (cancel_moved(cancel_word, epoch) || preempted(ctr_start + done)) break;
     const bool lat = first && use_lat;
     const uint64_t cap = lat ? ctx->lat_max : (uint64_t)1 << 30;
     const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(step, cap), ctr_count - done);
@@ -739,8 +772,11 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
         // records its digest): one dispatch with the constants as kernel
         // argument, about half the latency of K2's copy-in / hash / copy-out.
         const pow_stats keep = ctx->stats;
-        ctx->watch_epoch = false;  // the winner is hashed even if the epoch moves now
-        if (int rc = run_search_lat(ctx, ctr, 1, 0, true, 1)) return rc;
+        ctx->watch_epoch = false;  // the winner is hashed even if the epoch moves now ...
+        ctx->board_off = true;     // ... or a peer has published a solution
+        const int rc = run_search_lat(ctx, ctr, 1, 0, true, 1);
+        ctx->board_off = false;
+        if (rc) return rc;
         ctx->stats = keep;
         const PowResult& w = *ctx->h_res;
         if (w.nhit < 1 || w.hit[0].rel != 0) return fail(POW_EHIP, "winner re-hash recorded no digest");
@@ -749,8 +785,11 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
       memcpy(out->block_hash, hx, 65);  // strcpy semantics (node.cpp:318)
       if (found_ctr) *found_ctr = ctr;
       if (hashes_done) *hashes_done = ctx->stats.hashes;
+      // The kernel already stored its hits; this is the exact result.
+      if (ctx->board) pow_board_post(ctx->board, ctx->board_slot, ctx->board_tag, ctr);
       return 1;
     }
+    if (preempted(ctr_start + done)) break;
     step = any ? 1ull << 30 : std::min<uint64_t>(n * 4, 1ull << 30);
   }
   if (hashes_done) *hashes_done = ctx->stats.hashes;
@@ -778,6 +817,28 @@ int pow_cancel(pow_ctx* ctx, uint32_t epoch) {
   __atomic_store_n(ctx->h_epoch, epoch, __ATOMIC_SEQ_CST);
   ctx->armed.store(true, std::memory_order_release);
   return POW_OK;
+}
+
+int pow_board_bind(pow_ctx* ctx, pow_board* b, int slot, uint32_t tag) {
+  if (!ctx) return fail(POW_EINVAL, "null ctx");
+  if (!b) {
+    ctx->board = nullptr;
+    ctx->board_dev = nullptr;
+    ctx->board_slot = -1;
+    ctx->board_tag = 0;
+    return POW_OK;
+  }
+  if (slot < 0 || slot >= pow_board_nslots(b)) return fail(POW_EINVAL, "slot %d of %d", slot, pow_board_nslots(b));
+  if (tag < 1 || tag > POW_BOARD_MAX_TAG) return fail(POW_EINVAL, "tag must be 1..1023");
+  if (int rc = set_dev(ctx)) return rc;
+  if (int rc = pow_board_register(b)) return rc;
+  void* d = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&d, pow_board_host_slots(b), 0));
+  ctx->board = b;
+  ctx->board_dev = (const unsigned long long*)d;
+  ctx->board_slot = slot;
+  ctx->board_tag = tag;
+  return pow_board_post(b, slot, tag, UINT64_MAX);  // nothing found yet in this search
 }
 
 int pow_dev_alloc(pow_ctx* ctx, size_t bytes, void** out) {

@@ -14,6 +14,13 @@
 // success (send_block_to_everyone, node.cpp:260-273).  This is the
 // cooperative form of that search: one template, several GPUs.
 //
+// Inside a round, the ranks of one node also share a stop board
+// (pow_board.cpp), named after the RCCL id: a rank's hit reaches the other
+// GPUs' running kernels within one inner step, so they stop mining instead of
+// finishing their shards (any-mode: every peer stops; lowest mode: peers stop
+// the counters above the hit).  The round's all-reduce then only agrees on a
+// winner the ranks already know of.
+//
 // RCCL is opened with dlopen at first use, so libpow_gpu.so has no link-time
 // dependency on it and the single-GPU entry points never load it.
 #include <dlfcn.h>
@@ -84,6 +91,8 @@ struct pow_group {
   ncclComm_t comm = nullptr;
   uint64_t* d_buf = nullptr;  // kMaxWords device words: the all-reduce operand
   uint64_t* h_buf = nullptr;  // pinned host mirror
+  pow_board* board = nullptr; // the node's stop board (null: more than 64 ranks, or none available)
+  uint32_t searches = 0;      // searches so far: every rank counts the same (the calls are collective)
 };
 
 namespace {
@@ -102,6 +111,105 @@ int group_allreduce(pow_group* g, uint64_t* v, size_t n, ncclRedOp_t op) {
     return hip_fail("hipMemcpyAsync", e);
   if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail("hipStreamSynchronize", e);
   memcpy(v, g->h_buf, n * sizeof(uint64_t));
+  return POW_OK;
+}
+
+// The board's shared-memory name: from the RCCL id, the same on every rank.
+void board_name(const uint8_t id[POW_GROUP_ID_BYTES], char name[40]) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a
+  for (int i = 0; i < POW_GROUP_ID_BYTES; ++i) h = (h ^ id[i]) * 1099511628211ull;
+  snprintf(name, 40, "/pow_board_%016llx", (unsigned long long)h);
+}
+
+// Search tag of the next search (1..1023, the same on every rank).
+uint32_t next_tag(pow_group* g) { return 1u + (g->searches++ % POW_BOARD_MAX_TAG); }
+
+// Statistics of a multi-call search (pow_mine resets the ctx's per call).
+struct StatSum {
+  pow_stats s{};
+  void add(const pow_ctx* ctx) {
+    pow_stats t{};
+    pow_get_stats(ctx, &t);
+    s.kernel_ms += t.kernel_ms;
+    s.launches += t.launches;
+    s.hashes += t.hashes;
+  }
+};
+
+// The winner's block: nonce + block_hash through a one-counter pow_mine at
+// difficulty 0 (one latency-kernel dispatch that records the digest; the
+// board is unbound by then, so the peers' published hits do not stop it).
+int winner_block(pow_group* g, const pow_block* tmpl, uint64_t ctr, pow_block* out, StatSum& st) {
+  uint64_t c = 0;
+  const int rc = pow_mine(g->ctx, tmpl, ctr, 1, 0, nullptr, 0, out, &c, nullptr);
+  st.add(g->ctx);
+  if (rc < 0) return rc;
+  if (rc != 1 || c != ctr) return pow_set_error(POW_EHIP, "winner re-hash failed");
+  return POW_OK;
+}
+
+// Rounds of a collective search (both modes): every rank mines its static
+// shard of each round (with the board bound), then one all-reduce(min) of
+// {counter found, go, ok} picks the winner, spreads cancellation and failure.
+int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count, uint64_t round_size,
+                 bool adaptive, unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
+                 pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done, bool any) {
+  const uint64_t big = (uint64_t)g->nranks << 30;
+  const uint32_t tag = next_tag(g);
+  if (g->board)
+    if (int rc = pow_board_bind(g->ctx, g->board, g->rank, tag)) return rc;
+  struct Unbind {
+    pow_group* g;
+    ~Unbind() { pow_board_bind(g->ctx, nullptr, 0, 0); }
+  } unbind{g};
+  StatSum st;
+  if (hashes_done) *hashes_done = 0;
+  for (uint64_t done = 0; done < ctr_count;) {
+    const uint64_t n = std::min(round_size, ctr_count - done);
+    uint64_t s = 0, k = 0;
+    pow_group_partition(ctr_start + done, n, g->rank, g->nranks, &s, &k);
+    // {counter found by this rank (any: its first; lowest: its shard's lowest), go (0 = cancelled), ok (0 = failed)}
+    uint64_t v[3] = {UINT64_MAX, 1, 1};
+    int local_rc = POW_OK;
+    char local_err[512] = {0};
+    if (k) {
+      pow_block tmp;
+      uint64_t c = 0;
+      local_rc = any ? pow_mine_any(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, nullptr)
+                     : pow_mine(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, nullptr);
+      st.add(g->ctx);
+      if (local_rc == 1) v[0] = c;
+      if (local_rc < 0) {
+        v[2] = 0;
+        snprintf(local_err, sizeof local_err, "%s", pow_last_error());
+      }
+    }
+    if (cancel_moved(cancel_word, epoch)) v[1] = 0;
+    if (int rc = group_allreduce(g, v, 3, ncclMin)) return rc;
+    if (hashes_done) *hashes_done = st.s.hashes;
+    pow_ctx_set_stats(g->ctx, st.s);
+    if (v[2] == 0)  // every rank leaves the search together
+      return local_rc < 0 ? pow_set_error(local_rc, local_err) : pow_set_error(POW_ECOMM, "a peer rank failed");
+    if (v[1] == 0) return 0;  // cancelled on some rank
+    if (v[0] != UINT64_MAX) {
+      pow_board_bind(g->ctx, nullptr, 0, 0);
+      if (int rc = winner_block(g, tmpl, v[0], out, st)) return rc;
+      pow_ctx_set_stats(g->ctx, st.s);
+      if (found_ctr) *found_ctr = v[0];
+      return 1;
+    }
+    done += n;
+    if (adaptive) round_size = std::min<uint64_t>(big, round_size * 4);
+  }
+  return 0;
+}
+
+int check_args(const pow_group* g, const pow_block* tmpl, const pow_block* out, uint64_t ctr_start,
+               uint64_t ctr_count, unsigned diff_bits) {
+  if (!g || !tmpl || !out) return pow_set_error(POW_EINVAL, "null");
+  if (ctr_start >= POW_COUNTER_LIMIT || ctr_count > POW_COUNTER_LIMIT - ctr_start)
+    return pow_set_error(POW_EINVAL, "counter range past 62^9");
+  if (diff_bits > 256) return pow_set_error(POW_EINVAL, "difficulty > 256 bits");
   return POW_OK;
 }
 
@@ -149,9 +257,17 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
     pow_group_destroy(g);
     return hip_fail("group buffers", e);
   }
+  // The node's stop board: opened before the communicator, so that once
+  // ncclCommInitRank returns (every rank joined) every rank has it mapped and
+  // its name can go.  Without one (> 64 ranks, no shared memory) the ranks
+  // still stop together at the end of each round.
+  char name[40];
+  board_name(id, name);
+  if (nranks <= POW_BOARD_MAX_SLOTS && pow_board_open(name, nranks, &g->board) != POW_OK) g->board = nullptr;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   ncclResult_t r = R.comm_init_rank(&g->comm, nranks, u, rank);  // returns once every rank joined
+  pow_board_unlink(name);
   if (r != ncclSuccess) {
     g->comm = nullptr;
     pow_group_destroy(g);
@@ -165,6 +281,8 @@ void pow_group_destroy(pow_group* g) {
   if (!g) return;
   (void)hipSetDevice(pow_ctx_device(g->ctx));
   if (g->comm) (void)rccl().comm_destroy(g->comm);
+  pow_board_bind(g->ctx, nullptr, 0, 0);
+  pow_board_close(g->board);
   (void)hipFree(g->d_buf);
   if (g->h_buf) (void)hipHostFree(g->h_buf);
   delete g;
@@ -185,10 +303,7 @@ int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op) {
 int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
                    uint64_t round_size, unsigned diff_bits, const volatile uint32_t* cancel_word,
                    uint32_t epoch, pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
-  if (!g || !tmpl || !out) return pow_set_error(POW_EINVAL, "null");
-  if (ctr_start >= POW_COUNTER_LIMIT || ctr_count > POW_COUNTER_LIMIT - ctr_start)
-    return pow_set_error(POW_EINVAL, "counter range past 62^9");
-  if (diff_bits > 256) return pow_set_error(POW_EINVAL, "difficulty > 256 bits");
+  if (int rc = check_args(g, tmpl, out, ctr_start, ctr_count, diff_bits)) return rc;
   // Default (round_size = 0): adaptive rounds, as pow_mine's sub-rounds.  The
   // first round covers ~4x the expected trials (2^(d+2) counters, at least
   // 2^16 per GPU), later ones grow 4x up to 2^30 counters per GPU (~0.13 s at
@@ -201,46 +316,21 @@ int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint
     const unsigned dcap = diff_bits > 40 ? 40 : diff_bits;
     round_size = std::min<uint64_t>(big, std::max<uint64_t>((uint64_t)g->nranks << 16, 1ull << (dcap + 2)));
   }
-  uint64_t hashes = 0;
-  if (hashes_done) *hashes_done = 0;
-  for (uint64_t done = 0; done < ctr_count;) {
-    const uint64_t n = std::min(round_size, ctr_count - done);
-    uint64_t s = 0, k = 0;
-    pow_group_partition(ctr_start + done, n, g->rank, g->nranks, &s, &k);
-    // {lowest solving counter of this rank's shard, go (0 = cancelled), ok (0 = failed)}
-    uint64_t v[3] = {UINT64_MAX, 1, 1};
-    int local_rc = POW_OK;
-    char local_err[512] = {0};
-    if (k) {
-      pow_block tmp;
-      uint64_t c = 0, h = 0;
-      local_rc = pow_mine(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, &h);
-      hashes += h;
-      if (local_rc == 1) v[0] = c;
-      if (local_rc < 0) {
-        v[2] = 0;
-        snprintf(local_err, sizeof local_err, "%s", pow_last_error());
-      }
-    }
-    if (cancel_moved(cancel_word, epoch)) v[1] = 0;
-    if (int rc = group_allreduce(g, v, 3, ncclMin)) return rc;
-    if (hashes_done) *hashes_done = hashes;
-    if (v[2] == 0)  // every rank leaves the search together
-      return local_rc < 0 ? pow_set_error(local_rc, local_err) : pow_set_error(POW_ECOMM, "a peer rank failed");
-    if (v[1] == 0) return 0;  // cancelled on some rank
-    if (v[0] != UINT64_MAX) {
-      *out = *tmpl;
-      if (int rc = pow_nonce_from_counter(v[0], out->nonce)) return rc;
-      char hx[65];
-      if (int rc = pow_hash_block(g->ctx, out, nullptr, hx)) return rc;
-      memcpy(out->block_hash, hx, 65);  // strcpy semantics (node.cpp:318)
-      if (found_ctr) *found_ctr = v[0];
-      return 1;
-    }
-    done += n;
-    if (adaptive) round_size = std::min<uint64_t>(big, round_size * 4);
-  }
-  return 0;
+  return group_search(g, tmpl, ctr_start, ctr_count, round_size, adaptive, diff_bits, cancel_word, epoch, out,
+                      found_ctr, hashes_done, false);
+}
+
+int pow_group_mine_any(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
+                       uint64_t round_size, unsigned diff_bits, const volatile uint32_t* cancel_word,
+                       uint32_t epoch, pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done) {
+  if (int rc = check_args(g, tmpl, out, ctr_start, ctr_count, diff_bits)) return rc;
+  // Any-mode needs no growing rounds: pow_mine_any starts each shard with its
+  // latency kernel and a hit anywhere on the node stops every GPU through the
+  // board.  2^32 counters per rank per round (~0.5 s) keep the all-reduce,
+  // which also carries cancellation across nodes, rare.
+  if (round_size == 0) round_size = (uint64_t)g->nranks << 32;
+  return group_search(g, tmpl, ctr_start, ctr_count, round_size, false, diff_bits, cancel_word, epoch, out,
+                      found_ctr, hashes_done, true);
 }
 
 }  // extern "C"

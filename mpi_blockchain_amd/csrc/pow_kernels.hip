@@ -115,27 +115,60 @@ __device__ __forceinline__ void flush_tail(const uint32_t* wst, uint32_t nst, ui
   if (lane < nst && base + lane < tail_cap) tail[base + lane] = wst[lane];
 }
 
-// pow_cancel: has the caller's epoch moved past this launch's?  One sentinel
-// wave (workgroup 0, wave 0) reads the caller's epoch from mapped host memory
-// (one PCIe read per poll, so not every wave) and raises res->cancelled; every
-// wave reads that device word.  A memset or copy into device memory could not
-// do this: the copy engine's blit kernel waits for a free CU, and the mining
-// kernel holds them all.  Wave-uniform.
-__device__ __forceinline__ bool epoch_moved(uint32_t watch, const unsigned int* host_epoch, uint32_t launch_epoch,
-                                            unsigned int* cancelled) {
-  if (!watch) return false;
+// Should this wave stop for a reason outside its own launch?  Two sources:
+//   * pow_cancel: the caller's epoch (mapped host memory) moved off the
+//     launch's epoch;
+//   * a bound stop board: a peer (another GPU or context of the same search)
+//     published a solution below `lowest_abs`, the lowest absolute counter the
+//     wave would still compute (~0 in any-mode: any peer solution stops it).
+// Host memory is read by ONE sentinel wave (workgroup 0, wave 0: one PCIe
+// read per poll, not one per wave).  It raises device words every wave polls:
+// `cancelled`, and `peer_abs` = the lowest peer counter seen.  A memset or
+// copy into device memory could not do this: the copy engine's blit kernel
+// waits for a free CU, and the mining kernel holds them all.  Wave-uniform.
+__device__ __forceinline__ bool poll_stop(const PowWatch& w, unsigned int* cancelled, unsigned long long* peer_abs,
+                                          unsigned long long lowest_abs) {
+  const uint32_t watch = w.watch_epoch;
+  const unsigned long long* const board = w.board;
+  if (!watch && !board) return false;
   if (blockIdx.x == 0 && threadIdx.x < 64u) {
-    const unsigned int now = __hip_atomic_load(host_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if ((uint32_t)__builtin_amdgcn_readfirstlane(now) != launch_epoch) {
-      if (threadIdx.x == 0) __hip_atomic_store(cancelled, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return true;
+    const uint32_t lane = threadIdx.x;
+    if (watch) {
+      const unsigned int now = __hip_atomic_load(w.host_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((uint32_t)__builtin_amdgcn_readfirstlane(now) != w.launch_epoch && lane == 0)
+        __hip_atomic_store(cancelled, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (board) {
+      unsigned long long c = ~0ull;
+      if (lane < w.board_n && board + lane != w.board_mine) {
+        const unsigned long long v = __hip_atomic_load(board + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(v >> POW_BOARD_SHIFT) == w.board_tag && (v & POW_BOARD_NONE) != POW_BOARD_NONE)
+          c = v & POW_BOARD_NONE;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(c, off, 64);
+        c = o < c ? o : c;
+      }
+      if (lane == 0 && c != ~0ull) atomicMin(peer_abs, c);
     }
   }
-  return __builtin_amdgcn_readfirstlane(
-             __hip_atomic_load(cancelled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+  if (watch && __builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(cancelled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u)
+    return true;
+  return board && uniform64(__hip_atomic_load(peer_abs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < lowest_abs;
 }
-__device__ __forceinline__ bool epoch_moved(PowResult* res) {
-  return epoch_moved(res->watch_epoch, res->host_epoch, res->launch_epoch, &res->cancelled);
+
+// A hit of a mine launch goes to this context's board slot at once (system
+// scope, straight into host memory), so the peers' sentinels see it within
+// their next poll.  Several lanes may store: any stored value is a real
+// solution, and a peer only ever compares against it (a higher value than
+// this launch's lowest just stops the peers a little less eagerly).
+__device__ __forceinline__ void publish_hit(const PowWatch& w, unsigned long long rel) {
+  unsigned long long* const mine = w.board_mine;
+  if (mine)
+    __hip_atomic_store(mine, ((unsigned long long)w.board_tag << POW_BOARD_SHIFT) | (w.abs_start + rel),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Leading zero bits of the 256-bit digest H[0..7] >= d  (d > 32 path only).
@@ -189,7 +222,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       long long lo = (long long)rbase * 62 - (long long)L.off0;
       if (MODE == 2 && f != ~0ull) break;
       if (lo > 0 && f < (unsigned long long)lo) break;
-      if (epoch_moved(res)) break;
+      if (poll_stop(res->watch, &res->cancelled, &res->peer_abs,
+                    MODE == 2 ? ~0ull : res->watch.abs_start + (lo > 0 ? (unsigned long long)lo : 0ull)))
+        break;
     }
     const uint32_t r = rbase + lane;
 
@@ -238,7 +273,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         f = uniform64(f);
         long long lo = (long long)rbase * 62 + j - (long long)L.off0;
         if (lo > 0 && f < (unsigned long long)lo) break;
-        if (epoch_moved(res)) {
+        // (cancelled, or a peer holds a lower counter: every later chunk is higher still)
+        if (poll_stop(res->watch, &res->cancelled, &res->peer_abs,
+                      res->watch.abs_start + (lo > 0 ? (unsigned long long)lo : 0ull))) {
           stop = true;
           break;
         }
@@ -246,7 +283,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       if (MODE == 2 && j != 0) {
         unsigned long long f =
             __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (uniform64(f) != ~0ull || epoch_moved(res)) {
+        if (uniform64(f) != ~0ull || poll_stop(res->watch, &res->cancelled, &res->peer_abs, ~0ull)) {
           stop = true;
           break;
         }
@@ -326,7 +363,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         if (__builtin_expect(hit, 0)) {
           const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
           // rel < count also rejects j < off0 at r = 0 (wraps) and lanes past the end
-          if (rel < L.count) atomicMin(&res->min_rel, rel);
+          if (rel < L.count) {
+            atomicMin(&res->min_rel, rel);
+            publish_hit(res->watch, rel);
+          }
         }
       } else {
         bool ok = false;
@@ -425,7 +465,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     f = uniform64(f);
     if (ANY ? f != ~0ull : f < (unsigned long long)q) break;
-    if (epoch_moved(L.watch_epoch, L.host_epoch, L.launch_epoch, &res->cancelled)) break;
+    if (poll_stop(L.watch, &res->cancelled, &res->peer_abs, ANY ? ~0ull : L.watch.abs_start + q)) break;
     ++iters;
     const uint32_t rel = q + lane;
     uint32_t dg[9];
@@ -487,6 +527,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     if (FULL && hit) hit = full_test(D, L.diff);
     if (__builtin_expect(hit, 0) && (unsigned long long)rel < L.count) {
       atomicMin(&res->min_rel, (unsigned long long)rel);
+      publish_hit(L.watch, rel);
       const uint32_t slot = atomicAdd(&res->nhit, 1u);
       if (slot < POW_HITS) {
         res->hit[slot].rel = rel;
@@ -531,6 +572,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         res->hashes = 0;
         res->nhit = 0;
         res->cancelled = 0;
+        res->peer_abs = ~0ull;
       }
       __threadfence_system();
     }

@@ -56,17 +56,37 @@ struct PowConsts {
 #define PC_K (PC_W3 + POW_J)
 #define PC_WRAW (PC_K + 64)
 
-// Launch parameters of one kernel dispatch.
+// Stop board slots (include/pow_gpu.h "cross-GPU stop board"): one u64 per
+// rank in host memory every GPU of the node maps; bits 63..54 hold the
+// search tag, bits 53..0 an absolute counter (62^9 < 2^54), all ones = none.
+#define POW_BOARD_SHIFT 54
+#define POW_BOARD_NONE ((1ull << POW_BOARD_SHIFT) - 1)
+
+// What a mine launch watches besides its own result words (both kernels):
+//   * the caller's cancel epoch (pow_cancel), in mapped host memory;
+//   * the peers' slots of a bound stop board, and it publishes its own hits
+//     to its slot.  Only one sentinel wave per launch reads host memory; it
+//     raises device words (`cancelled`, `peer_abs` of the result) that every
+//     wave polls.
+struct PowWatch {
+  const unsigned int* host_epoch;     // pow_cancel's word (device address of mapped host memory)
+  const unsigned long long* board;    // null: no board bound
+  unsigned long long* board_mine;     // this ctx's slot (a hit is stored here at system scope)
+  unsigned long long abs_start;       // absolute counter of relative counter 0
+  uint32_t watch_epoch;               // pow_cancel armed: watch host_epoch against launch_epoch
+  uint32_t launch_epoch;
+  uint32_t board_n;                   // slots (<= 64: one lane each)
+  uint32_t board_tag;                 // search tag of the bound search (1..1023)
+};
+
 // Launch parameters of the latency kernel (one counter per lane).
 struct PowLaunchLat {
   uint32_t base_digit[9];  // base-62 digits of ctr_start (nonce[0..8])
   uint32_t thr;            // as PowLaunch
   uint32_t diff;
-  uint32_t watch_epoch;    // pow_cancel armed: watch host_epoch against launch_epoch
-  uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
-  const unsigned int* host_epoch;
-  uint32_t launch_epoch;
   uint32_t pad;
+  uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
+  PowWatch watch;
   const PowConsts* consts_dev;  // null: read the by-value copy in the kernarg segment
 };
 
@@ -102,11 +122,9 @@ struct PowResult {
   unsigned int* tail_buf;      // sweep: each wave's last < 32 solutions (appended by the host);
                                // read from here at wave exit, not held in SGPRs all kernel long
   unsigned int nhit;           // latency kernel: solutions found (the first POW_HITS are in hit[])
-  unsigned int launch_epoch;   // mine modes: the caller's epoch for this launch ...
-  unsigned int watch_epoch;    // ... watched when nonzero (pow_cancel armed):
-  const unsigned int* host_epoch;  // the caller's current epoch, in mapped host memory
   unsigned int cancelled;      // set once a sentinel wave saw host_epoch != launch_epoch
-  unsigned int pad3;
+  unsigned long long peer_abs; // lowest counter a peer published on the board (sentinel wave), ~0 = none
+  PowWatch watch;              // K1 mine modes (K1' takes it in its launch parameters)
   PowHit hit[POW_HITS];
 };
 
@@ -130,5 +148,13 @@ void* pow_ctx_stream(const struct pow_ctx* ctx);  // the ctx's hipStream_t
 int pow_set_error(int code, const char* msg);
 // True once another thread moved the caller's cancel word off `epoch` (acquire load).
 bool cancel_moved(const volatile uint32_t* cancel_word, uint32_t epoch);
+// Sum of per-call statistics kept across several calls (pow_group rounds).
+struct pow_stats;
+void pow_ctx_set_stats(struct pow_ctx* ctx, const struct pow_stats& s);
+// Stop board internals (pow_board.cpp).
+struct pow_board;
+uint64_t* pow_board_host_slots(const struct pow_board* b);
+int pow_board_nslots(const struct pow_board* b);
+int pow_board_register(struct pow_board* b);  // hipHostRegister once (first bind)
 }
 #endif

@@ -114,6 +114,13 @@ class GpuMiner:
     def epoch(self) -> int:
         return self._cancel.value
 
+    def bind_board(self, board: "StopBoard | None", slot: int = 0, tag: int = 1) -> None:
+        """Join a search shared with other GPUs / contexts (pow_board_bind):
+        this miner's hits go to `slot` of `board`, and its mine calls stop as
+        soon as a peer slot of the same `tag` makes its remaining counters
+        moot.  board=None unbinds."""
+        check(self.L.pow_board_bind(self.ctx, board.ptr if board is not None else None, slot, tag))
+
     def mine(self, tmpl: Block, start: int = 0, count: int = 1 << 40, difficulty: int = DEFAULT_DIFFICULTY,
              epoch: int | None = None, any_solution: bool = False) -> MineResult | None:
         """Lowest solving counter in [start, start+count) (pow_mine), or the
@@ -150,6 +157,44 @@ class GpuMiner:
         return n.value, (None if mn.value == 0xFFFFFFFFFFFFFFFF else mn.value)
 
 
+class StopBoard:
+    """Cross-GPU stop board (include/pow_gpu.h): one slot per rank of a shared
+    search, in host memory every GPU of the node maps.  name=None: private to
+    this process; name="/x": POSIX shared memory, shared by every process of
+    the node that opens it."""
+
+    NONE = None
+
+    def __init__(self, nslots: int, name: str | None = None):
+        self.L = load()
+        self.name = name
+        self.ptr = ctypes.c_void_p()
+        check(self.L.pow_board_open(name.encode() if name else None, nslots, ctypes.byref(self.ptr)))
+
+    def post(self, slot: int, tag: int, counter: int | None) -> None:
+        check(self.L.pow_board_post(self.ptr, slot, tag, 0xFFFFFFFFFFFFFFFF if counter is None else counter))
+
+    def peek(self, except_slot: int, tag: int) -> int | None:
+        v = ctypes.c_uint64()
+        check(self.L.pow_board_peek(self.ptr, except_slot, tag, ctypes.byref(v)))
+        return None if v.value == 0xFFFFFFFFFFFFFFFF else v.value
+
+    def unlink(self) -> None:
+        if self.name:
+            check(self.L.pow_board_unlink(self.name.encode()))
+
+    def close(self) -> None:
+        if self.ptr:
+            self.L.pow_board_close(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 class DeviceBuffer:
     """Device memory owned by a GpuMiner's context (raw pointer for the C ABI)."""
 
@@ -182,5 +227,5 @@ def block_hex(b: Block) -> str:
     return field(b, "block_hash").split(b"\0", 1)[0].decode()
 
 
-__all__ = ["GpuMiner", "DeviceBuffer", "MineResult", "refresh_template", "proof_of_work_round", "block_hex",
+__all__ = ["GpuMiner", "DeviceBuffer", "StopBoard", "MineResult", "refresh_template", "proof_of_work_round", "block_hex",
            "nonce_from_counter"]

@@ -124,9 +124,12 @@ class RcclGroup:
         return list(arr)
 
     def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
-             epoch: int | None = None):
-        """Lowest solving counter of [start, start+count) over all ranks (the
-        same MineResult on every rank; ``hashes`` = this rank's trials)."""
+             epoch: int | None = None, any_solution: bool = False):
+        """Lowest solving counter of [start, start+count) over all ranks
+        (pow_group_mine), or with ``any_solution`` the first solution any GPU
+        finds (pow_group_mine_any: the finder stops the node's other GPUs
+        through the stop board).  The same MineResult on every rank;
+        ``hashes`` and ``kernel_ms`` are this rank's, summed over the rounds."""
         from ._lib import Block, check
         from .miner import MineResult
 
@@ -134,9 +137,10 @@ class RcclGroup:
         ctr, hashes = ctypes.c_uint64(), ctypes.c_uint64()
         m = self.miner
         ep = m.epoch if epoch is None else epoch
-        rc = check(m.L.pow_group_mine(self.g, ctypes.byref(tmpl), start, count, round_size, difficulty,
-                                      ctypes.byref(m._cancel), ep, ctypes.byref(out), ctypes.byref(ctr),
-                                      ctypes.byref(hashes)))
+        fn = m.L.pow_group_mine_any if any_solution else m.L.pow_group_mine
+        rc = check(fn(self.g, ctypes.byref(tmpl), start, count, round_size, difficulty,
+                      ctypes.byref(m._cancel), ep, ctypes.byref(out), ctypes.byref(ctr),
+                      ctypes.byref(hashes)))
         if rc == 0:
             return None
         return MineResult(out, ctr.value, hashes.value, m.stats()["kernel_ms"])
@@ -163,16 +167,51 @@ def native_partition(start: int, count: int, rank: int, world: int) -> tuple[int
 
 
 class ShardedMiner:
-    """GPU-backed sharded search for one rank (one GPU per process)."""
+    """GPU-backed sharded search for one rank (one GPU per process) over
+    torch.distributed.  With ``board=True`` the ranks of one node also share a
+    stop board (its name broadcast from rank 0), so a rank's hit stops the
+    others inside their running launches, as pow_group_* do natively."""
 
-    def __init__(self, miner, rank: int, world: int, device=None, group=None):
+    def __init__(self, miner, rank: int, world: int, device=None, group=None, board: bool = False):
         self.miner, self.rank, self.world = miner, rank, world
         self.allreduce_min = torch_allreduce_min(device, group)
+        self.board, self._searches = None, 0
+        if board and world <= 64:
+            import os
+            import uuid
 
-    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0):
+            import torch.distributed as dist
+
+            from .miner import StopBoard
+
+            obj = [f"/pow_board_{os.getpid()}_{uuid.uuid4().hex[:12]}" if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            self.board = StopBoard(world, obj[0])
+            dist.barrier(group=group)  # every rank has it mapped: the name can go
+            self.board.unlink()
+
+    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
+             any_solution: bool = False):
+        """Lowest solving counter over all ranks, or (``any_solution``) the
+        lowest of the counters the ranks found first in the winning round."""
+        if self.board is not None:
+            self._searches += 1
+            self.miner.bind_board(self.board, self.rank, 1 + (self._searches - 1) % 1023)
+
         def search(s, n):
-            r = self.miner.mine(tmpl, s, n, difficulty)
+            r = self.miner.mine(tmpl, s, n, difficulty, any_solution=any_solution)
             return None if r is None else r.counter
 
-        return sharded_mine(search, self.allreduce_min, start, count, round_size, self.rank, self.world,
-                            difficulty)
+        try:
+            return sharded_mine(search, self.allreduce_min, start, count,
+                                (self.world << 32 if any_solution and not round_size else round_size),
+                                self.rank, self.world, difficulty)
+        finally:
+            if self.board is not None:
+                self.miner.bind_board(None)
+
+    def close(self) -> None:
+        if self.board is not None:
+            self.miner.bind_board(None)
+            self.board.close()
+            self.board = None

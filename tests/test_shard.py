@@ -158,3 +158,87 @@ def test_round_plan_adaptive():
             return O.mine(b, s, n, d)
         assert sharded_mine(search, lambda v: v, 0, 1 << 20, 0, 0, 1, d) == O.mine(b, 0, 1 << 20, d)
         assert sizes[0] == round_plan(1, d)[0] and all(y == 4 * x for x, y in zip(sizes, sizes[1:-1]))
+
+
+def test_board_host_protocol():
+    """The stop board's host side (no GPU): slots tagged per search, the
+    lowest peer counter, stale tags ignored, argument checks."""
+    from mpi_blockchain_amd import _lib
+    from mpi_blockchain_amd.miner import StopBoard
+
+    with StopBoard(4) as b:
+        assert b.peek(0, 1) is None  # fresh page: tag 0 everywhere
+        b.post(1, 1, 500)
+        b.post(2, 1, 300)
+        b.post(3, 2, 100)            # another search's tag
+        assert b.peek(0, 1) == 300 and b.peek(2, 1) == 500 and b.peek(0, 2) == 100
+        b.post(2, 1, None)           # "nothing found yet"
+        assert b.peek(0, 1) == 500
+        b.post(1, 1, 62**9 - 1)      # the largest counter fits the 54-bit field
+        assert b.peek(0, 1) == 62**9 - 1
+        with pytest.raises(_lib.PowError):
+            b.post(4, 1, 0)          # no such slot
+        with pytest.raises(_lib.PowError):
+            b.post(0, 0, 0)          # tag 0 is reserved (a fresh page)
+        with pytest.raises(_lib.PowError):
+            b.post(0, 1024, 0)
+    L = _lib.load()
+    import ctypes
+    p = ctypes.c_void_p()
+    assert L.pow_board_open(None, 0, ctypes.byref(p)) == _lib.POW_EINVAL
+    assert L.pow_board_open(None, 65, ctypes.byref(p)) == _lib.POW_EINVAL
+    assert L.pow_board_open(b"no-slash", 2, ctypes.byref(p)) == _lib.POW_EINVAL
+    assert L.pow_board_bind(None, None, 0, 1) == _lib.POW_EINVAL
+
+
+def _board_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpi_blockchain_amd.miner import StopBoard
+
+    import uuid
+
+    obj = [f"/pow_board_cputest_{os.getpid()}_{uuid.uuid4().hex[:8]}" if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    b = StopBoard(world, obj[0])
+    dist.barrier()
+    b.unlink()  # both mapped: the name can go, the page stays shared
+    seen = []
+    for tag in (1, 2):
+        b.post(rank, tag, None)
+        dist.barrier()
+        seen.append(b.peek(rank, tag))       # nobody found anything yet
+        dist.barrier()
+        if rank == 1:
+            b.post(1, tag, 1000 * tag + 7)   # rank 1's hit
+        dist.barrier()
+        seen.append(b.peek(rank, tag))
+        seen.append(b.peek(rank, 3 - tag))   # the other search's tag: stale or absent
+        dist.barrier()
+    q.put((rank, seen))
+    b.close()
+    dist.destroy_process_group()
+
+
+def test_board_named_world2():
+    """Two processes (gloo world 2) share a named board: rank 1's post is
+    what rank 0 peeks, per search tag; the name is unlinked after both mapped
+    it.  The GPU side (kernels polling it) is tests/test_board_gpu.py."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_board_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # rank 0: search 1: none, then 1007 (search 2's tag: absent); search 2: none, then
+    # 2007, and search 1's value is gone (one slot per rank holds the current search)
+    assert out[0] == [None, 1007, None, None, 2007, None]
+    assert out[1] == [None, None, None, None, None, None]  # its own slot is excluded
