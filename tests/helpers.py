@@ -22,3 +22,21 @@ def with_nonce(b: Block, nonce10: bytes) -> Block:
     ctypes.pointer(c)[0] = b
     set_field(c, "nonce", nonce10)
     return c
+
+
+def leading_zero_bits(hexd: str) -> int:
+    return 256 - int(hexd, 16).bit_length()
+
+
+def check_chain(entries, blocks: int, difficulty: int) -> bool:
+    """A logged chain (tip first): consecutive indices, linked, every hash
+    solving.  Returns True if it is complete (blocks..1, ending at genesis).
+    A rank killed by the first finisher's MPI_Abort (node.cpp:330) may leave
+    a partial dump; what it did write must still be consistent."""
+    idx = [e.index for e in entries]
+    assert idx == list(range(idx[0], idx[0] - len(idx), -1)) if idx else True
+    for cur, prev in zip(entries, entries[1:]):
+        assert cur.prev == prev.hash
+    for e in entries:
+        assert len(e.hash) == 64 and leading_zero_bits(e.hash) >= difficulty
+    return idx == list(range(blocks, 0, -1)) and entries[-1].prev == ""

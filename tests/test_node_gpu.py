@@ -10,6 +10,7 @@ import time
 
 import pytest
 
+from helpers import check_chain
 from mpi_blockchain_amd.build import mpi_available
 from mpi_blockchain_amd.node import run_network
 
@@ -17,24 +18,6 @@ pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not mpi_available(), reason="no MPI in this image")]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref")
-
-
-def leading_zero_bits(hexd: str) -> int:
-    return 256 - int(hexd, 16).bit_length()
-
-
-def check_chain(entries, blocks: int, difficulty: int) -> bool:
-    """A logged chain (tip first): consecutive indices, linked, every hash
-    solving.  Returns True if it is complete (blocks..1, ending at genesis).
-    A rank killed by the first finisher's MPI_Abort (node.cpp:330) may leave
-    a partial dump; what it did write must still be consistent."""
-    idx = [e.index for e in entries]
-    assert idx == list(range(idx[0], idx[0] - len(idx), -1)) if idx else True
-    for cur, prev in zip(entries, entries[1:]):
-        assert cur.prev == prev.hash
-    for e in entries:
-        assert len(e.hash) == 64 and leading_zero_bits(e.hash) >= difficulty
-    return idx == list(range(blocks, 0, -1)) and entries[-1].prev == ""
 
 
 FORK_MSGS = ("Perdí la carrera", "Conflicto suave", "TAG_CHAIN_HASH")
