@@ -11,9 +11,15 @@ Workload (BASELINE config 2, one step): the deterministic counter sweep of
 created_at=1700000000, prev = 256 zero bytes) at difficulty 9 bits; every
 solving counter is written to a device buffer (~8.39 M per step).  With N GPUs
 each rank sweeps its own 2^32-counter shard [rank*2^32, (rank+1)*2^32) (weak
-scaling) and one 8-byte all-reduce(MIN) of the lowest solving counter + an
-all-reduce(SUM) of the counts over RCCL picks the winner, as a sharded search
-round does (mpi_blockchain_amd/shard.py).
+scaling) and an all-reduce(MIN) of the lowest solving counter + an
+all-reduce(SUM) of the counts picks the winner, as a sharded search round
+does.  The collectives are the library's own (pow_group_allreduce_u64: RCCL
+called from C++, mpi_blockchain_amd/csrc/pow_group.cpp), not torch's.
+
+Config 4's cooperative search is measured beside it (outside the timed
+region): `group_search` = time-to-block of pow_group_mine_any over all N GPUs
+(every GPU mines a static shard of one template; the first hit stops the
+others through the stop board; one all-reduce agrees on the winner).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -85,21 +91,27 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
         use_mpi = mpi_available()
     except Exception:
         use_mpi = False
-    for flav in ("O2", "O0"):
+    # With a CPU quota below the affinity mask, also one rank per CPU of the quota
+    # (the reference loop on the CPU time the job actually gets, without throttling).
+    runs = [("O2", ranks), ("O0", ranks)]
+    if quota and int(quota) < ranks:
+        runs.append(("O2_at_quota", max(1, int(quota))))
+    for key, np_ in runs:
+        flav = key[:2]
         mpi_exe = os.path.join(ROOT, "oracle", "_ref", f"ref_cpu_bench_mpi_{flav}")
         exe = os.path.join(ROOT, "oracle", "_ref", f"ref_cpu_bench_{flav}")
         try:
             if use_mpi and os.path.exists(mpi_exe):
-                cmd, how = ["timeout", "-k", "10", "180", MPIEXEC, "-np", str(ranks), mpi_exe, str(seconds)], "mpi"
+                cmd, how = ["timeout", "-k", "10", "180", MPIEXEC, "-np", str(np_), mpi_exe, str(seconds)], "mpi"
                 r = subprocess.run(cmd, capture_output=True, text=True, check=True, env=mpi_env(), cwd="/tmp")
             elif os.path.exists(exe):
-                cmd, how = [exe, str(ranks), str(seconds)], "fork"
+                cmd, how = [exe, str(np_), str(seconds)], "fork"
                 r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, check=True)
             else:
                 continue
-            out[flav] = json.loads(r.stdout.strip().splitlines()[-1])
+            out[key] = json.loads(r.stdout.strip().splitlines()[-1])
         except Exception as e:  # pragma: no cover
-            out[flav] = {"error": str(e)[-300:]}
+            out[key] = {"error": str(e)[-300:]}
     if "O2" in out and "trials_per_s" in out["O2"]:
         o2 = out["O2"]
         launch = (f"mpiexec -np {ranks} (one MPI rank per CPU)" if how == "mpi"
@@ -114,6 +126,12 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
         if "O0" in out and "trials_per_s" in out["O0"]:
             res["as_shipped_O0"] = round(out["O0"]["trials_per_s"], 1)
             res["as_shipped_O0_per_usable_cpu"] = round(out["O0"]["trials_per_s"] / usable, 1)
+        if "O2_at_quota" in out and "trials_per_s" in out["O2_at_quota"]:
+            q = out["O2_at_quota"]
+            res["at_cpu_quota"] = {"ranks": q.get("ranks", q.get("procs")), "value": round(q["trials_per_s"], 1),
+                                   "per_rank": round(q["trials_per_s"] / max(1, q.get("ranks", q.get("procs", 1))), 1),
+                                   "note": "-O2, one rank per CPU of the cgroup quota: 256 ranks on 16 CPUs' worth "
+                                           "of time lose to throttling"}
         res["host_cpus"] = dict(host, ranks=ranks, usable=usable)
         return res
     # restatement fallback ("port")
@@ -136,12 +154,16 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
         return {"error": str(e)}
 
 
+PMC_SUMMARY = os.path.join("profiles", "r02", "final", "pmc_summary.json")
+
+
 def pmc_traffic():
-    """HBM bytes per dispatch of this workload from the committed rocprofv3
-    PMC summary (tools/profile_round.sh + tools/pmc_summary.py)."""
-    p = os.path.join(ROOT, "profiles", "r01", "final", "pmc_summary.json")
+    """HBM bytes per dispatch of this workload, NOT measured in this run: PMC
+    counters need their own rocprofv3 passes (tools/profile_round.sh +
+    tools/pmc_summary.py), so the committed summary of those passes over the
+    same command and build is read back and labelled as such."""
     try:
-        return int(json.load(open(p))["hbm_bytes_per_dispatch"]["total"])
+        return int(json.load(open(os.path.join(ROOT, PMC_SUMMARY)))["hbm_bytes_per_dispatch"]["total"])
     except Exception:
         return None
 
@@ -225,6 +247,37 @@ def ladder(miner, n_templates: int = 101, rungs=(9, 13, 17, 21, 25)) -> dict:
     return out
 
 
+def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 21) -> dict:
+    """BASELINE config 4, cooperative form: time-to-block of pow_group_mine_any
+    over every GPU of the job (collective; the same templates on every rank).
+    Each rank mines its static shard; the first hit stops the node's other
+    GPUs inside their launches (stop board) and one all-reduce agrees on the
+    winner.  Expected trials per block 2^d; strong scaling in N."""
+    import random
+
+    from mpi_blockchain_amd.block import make_block
+
+    rng = random.Random(1)
+    times, hashes, counters = [], [], []
+    for _ in range(n_templates):
+        b = make_block(rng.randrange(1, 1 << 16), 0, 9, 1700000000 + rng.randrange(256),
+                       bytes(rng.randrange(256) for _ in range(32)).hex().encode())
+        group.allreduce([0], "sum")  # line the ranks up
+        t = time.perf_counter()
+        r = group.mine(b, 0, 1 << 48, d, any_solution=True)
+        times.append(time.perf_counter() - t)
+        hashes.append(group.allreduce([r.hashes if r else 0], "sum")[0])
+        counters.append(r.counter if r else None)
+    tot_t = sum(times)
+    return {"difficulty_bits": d, "templates": n_templates, "n_gpus": world,
+            "time_to_block_ms_median": round(1e3 * statistics.median(times), 3),
+            "time_to_block_ms_mean": round(1e3 * tot_t / n_templates, 3),
+            "expected_hashes": 2 ** d, "hashes_all_ranks_mean": int(sum(hashes) / n_templates),
+            "hashes_per_s_all_ranks": round(sum(hashes) / tot_t, 1),
+            "note": "pow_group_mine_any over all GPUs (static shards, stop board, one all-reduce per round); "
+                    "hashes include the trials peers ran before the winner's hit reached them"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,6 +288,7 @@ def main():
     ap.add_argument("--no-ladder", action="store_true")
     ap.add_argument("--no-peak", action="store_true")
     ap.add_argument("--no-protocol", action="store_true")
+    ap.add_argument("--no-group-search", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -259,15 +313,27 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
+    from mpi_blockchain_amd.shard import RcclGroup
 
     miner = GpuMiner(local)
+    rehearsal = os.environ.get("BENCH_REHEARSAL") == "1"
+    # The library's own RCCL communicator (the id travels over torch.distributed);
+    # at N = 1 a one-rank group, used only by the group_search measurement.
+    group, group_err = None, None
+    if not rehearsal:
+        try:
+            group = RcclGroup.from_torch(miner) if dist is not None else \
+                RcclGroup(miner, 0, 1, RcclGroup.make_unique_id())
+        except Exception as e:  # pragma: no cover - fall back to torch's collectives, say so
+            group_err = f"pow_group_init failed ({e}); torch.distributed collectives used instead"
+            group = None
     info = miner.device_info()
     tmpl = s0_block()
     d = args.difficulty
     start = rank * WINDOW
     cap = 12_000_000  # > 2^32 / 2^9 * 1.4
     buf = DeviceBuffer(miner, 4 * cap)
-    if dist is not None:
+    if dist is not None and group is None:
         red = torch.zeros(2, dtype=torch.int64, device=f"cuda:{local}")
 
     kernel_ms = []
@@ -278,7 +344,11 @@ def main():
         n, mn = miner.sweep_count(tmpl, start, WINDOW, d, dev_out=buf, cap=cap)
         kernel_ms.append(miner.stats()["kernel_ms"])
         local_last[0] = (n, mn)
-        if dist is not None:
+        if dist is not None and group is not None:  # RCCL through pow_group_allreduce_u64
+            lo = group.allreduce([mn if mn is not None else (1 << 64) - 1], "min")[0]
+            tot = group.allreduce([n], "sum")[0]
+            return tot, lo
+        if dist is not None:  # rehearsal (several ranks share one GPU over gloo), or no native group
             red[0] = mn if mn is not None else (1 << 63) - 1
             dist.all_reduce(red[0:1], op=dist.ReduceOp.MIN)
             red[1] = n
@@ -312,12 +382,21 @@ def main():
     if dist is not None:
         per_rank = [None] * world
         dist.all_gather_object(per_rank, local_last[0])
+    gsearch = None
+    if group is not None and not args.no_group_search:
+        try:
+            gsearch = group_search(group, rank, world)
+        except Exception as e:  # pragma: no cover - reported, not fatal: the headline is measured
+            gsearch = {"error": str(e)[-300:]}
     if rank != 0:
         buf.free()
+        if group is not None:
+            group.close()
         dist.destroy_process_group()
         return
-    collective = (f"{'rccl' if dist.get_backend() == 'nccl' else dist.get_backend()} all_reduce(min,sum) per step"
-                  if dist is not None else "none (single process)")
+    collective = ("rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if group is not None and world > 1
+                  else f"{dist.get_backend()} all_reduce(min,sum) per step via torch.distributed" if dist is not None
+                  else "none (single process)")
 
     kms = statistics.mean(kernel_ms) if kernel_ms else float("nan")
     value = world * WINDOW * args.steps / el
@@ -367,9 +446,10 @@ def main():
                      "unit": "Tops/s", "frac": round(achieved / peak["nominal_tops"], 4),
                      "traffic": pmc_traffic(), "algorithmic_bytes": 4 * (last[0] or 0),
                      "ops_per_hash": OPS_PER_HASH, "peak_detail": peak,
+                     "traffic_source": f"{PMC_SUMMARY} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
+                                       "command, median per dispatch; not measured in this run)",
                      "note": ("achieved = 2^32 hashes x 5000 int32 ops / mean HIP-event kernel time; "
-                              "traffic = FETCH_SIZE+WRITE_SIZE bytes per dispatch of the same workload "
-                              "(profiles/r01/final/pmc_summary.json, separate rocprofv3 --pmc passes)")},
+                              "traffic = FETCH_SIZE+WRITE_SIZE bytes per dispatch of the same workload")},
         "device": info,
         "parity": parity,
     }
@@ -377,9 +457,15 @@ def main():
         res["cpu_baseline"] = cpu_baseline()
     if world == 1 and not args.no_ladder:
         res["ladder"] = ladder(miner)
+    if gsearch is not None:
+        res["group_search"] = gsearch
+    if group_err:
+        res["group_error"] = group_err
     if world == 1 and not args.no_protocol:
         res["protocol"] = protocol_runs()
     buf.free()
+    if group is not None:
+        group.close()
     print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -29,6 +29,7 @@ if kt:
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
     out["dispatches"] = len(rows)
     out["avg_ns"] = sum(durs) / len(durs)
+    out["durations_ns"] = durs
     out["vgpr"], out["sgpr"] = rows[0]["VGPR_Count"], rows[0]["SGPR_Count"]
     out["grid"] = rows[0].get("Grid_Size_X") or rows[0].get("Grid_Size")
 
@@ -40,8 +41,11 @@ for f in glob.glob(os.path.join(root, f"{tag}_pmc*", "*counter_collection.csv"))
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (d, c), v in per.items():
         counters[c].append(v)
-avg = {c: sum(v) / len(v) for c, v in counters.items()}
+# Median per dispatch: an occasional dispatch overlaps another process's work
+# on the box (one FETCH_SIZE reading of 80 MB among 0.35 MB ones in r02).
+avg = {c: sorted(v)[len(v) // 2] for c, v in counters.items()}
 out["counters"] = avg
+out["per_dispatch"] = {c: v for c, v in counters.items()}
 t = out.get("avg_ns")
 if "SQ_INSTS_VALU" in avg:
     out["valu_instr_per_hash"] = avg["SQ_INSTS_VALU"] * 64 / hashes
