@@ -190,7 +190,23 @@ def protocol_runs() -> dict:
                                    env=mpi_env(), capture_output=True, text=True)
                 out["reference_np4_d9_wall_s"] = round(time.perf_counter() - t, 3)
                 out["reference_rc"] = p.returncode
-        for d in (9, 25):
+        # config 1 at d = 17 (oracle/Makefile: the reference with
+        # block.h's DEFAULT_DIFFICULTY line set to 17) for an aggregate CPU rate:
+        # 10 blocks x 2^17 expected trials / wall.  Each reference rank busy-polls a
+        # second core in MPI_Recv: 4 ranks occupy 8 CPUs.
+        ref17 = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref_d17")
+        if os.path.exists(ref17):
+            with tempfile.TemporaryDirectory() as td:
+                t = time.perf_counter()
+                p = subprocess.run(["timeout", "-k", "5", "120", MPIEXEC, "-np", "4", ref17], cwd=td,
+                                   env=mpi_env(), capture_output=True, text=True)
+                w = time.perf_counter() - t
+                out["reference_np4_d17_wall_s"] = round(w, 3)
+                out["reference_np4_d17_rc"] = p.returncode
+                out["reference_np4_d17_trials_per_s_est"] = round(10 * 2 ** 17 / w, 1)
+        else:
+            out["reference_np4_d17"] = "unmeasured: oracle/_ref/blockchain_ref_d17 not built"
+        for d in (9, 17, 25):
             with tempfile.TemporaryDirectory() as td:
                 t = time.perf_counter()
                 run = run_network(4, td, difficulty=d, blocks=10, timeout=180)

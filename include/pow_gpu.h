@@ -155,7 +155,8 @@ int pow_mine_any(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64
  * as (counter - ctr_start), ascending.  *n_found = number of solutions
  * (also when it exceeds cap, in which case POW_ENOSPC is returned and the
  * first `cap` entries are an unspecified subset).  out_ctrs may be NULL when
- * cap == 0 (count only).  Returns POW_OK. */
+ * cap == 0 (count only).  cap <= 2^31 - 1 (the list is sorted on the device;
+ * POW_EINVAL above).  Returns POW_OK. */
 int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
               unsigned diff_bits, uint32_t* out_ctrs, size_t cap, size_t* n_found);
 

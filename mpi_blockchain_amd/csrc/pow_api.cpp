@@ -656,11 +656,11 @@ int pow_sweep_device(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
 
 int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
               unsigned diff_bits, uint32_t* out_ctrs, size_t cap, size_t* n_found) {
+  // The device radix sort takes a signed 32-bit item count (hipCUB).
+  if (cap > 0x7FFFFFFFu) return fail(POW_EINVAL, "cap %zu > 2^31-1 (the host-list form sorts on the device)", cap);
   if (!ctx || !n_found) return fail(POW_EINVAL, "null");
   if (cap && !out_ctrs) return fail(POW_EINVAL, "cap without buffer");
   if (int rc = set_dev(ctx)) return rc;
-  // The device radix sort takes a signed 32-bit item count (hipCUB).
-  if (cap > 0x7FFFFFFFu) return fail(POW_EINVAL, "cap %zu > 2^31-1 (the host-list form sorts on the device)", cap);
   if (cap > ctx->out_cap) {
     (void)hipFree(ctx->d_out);
     (void)hipFree(ctx->d_alt);

@@ -96,3 +96,21 @@ def test_null_arguments_rejected():
     n = ctypes.c_size_t()
     assert L.pow_sweep(None, ctypes.byref(b), 0, 1, 9, None, 0, ctypes.byref(n)) == _lib.POW_EINVAL
     assert L.pow_nonce_from_counter(0, None) == _lib.POW_EINVAL
+
+
+def test_sweep_cap_limit():
+    """pow_sweep sorts its list on the device (hipCUB takes a signed 32-bit
+    count): a cap of 2^31 or more is rejected before any HIP call, and the
+    Python mirror's default cap never reaches it (2^32 window at d <= 1)."""
+    L = _lib.load()
+    b = make_block()
+    n = ctypes.c_size_t()
+    for cap in (1 << 31, (1 << 32) - 1, 1 << 40):
+        assert L.pow_sweep(None, ctypes.byref(b), 0, 1 << 32, 0, None, cap, ctypes.byref(n)) == _lib.POW_EINVAL
+        assert b"2^31-1" in L.pow_last_error()
+    import inspect
+
+    from mpi_blockchain_amd.miner import GpuMiner
+
+    src = inspect.getsource(GpuMiner.sweep)
+    assert "(1 << 31) - 1" in src

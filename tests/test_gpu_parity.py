@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from mpi_blockchain_amd._lib import COUNTER_LIMIT, PowError
-from mpi_blockchain_amd.block import block_to_str, field, nonce_from_counter
+from mpi_blockchain_amd.block import block_to_str, field, make_block, nonce_from_counter
 from mpi_blockchain_amd.miner import GpuMiner, block_hex, refresh_template
 
 from helpers import block_from_random, block_from_template, with_nonce
@@ -379,3 +379,15 @@ def test_random_templates_vs_oracle(miner):
         got = miner.sweep(make_block(idx, own, dif, cat, prev), start, count, d)
         want, n = O.sweep(make_oblock(idx, own, dif, cat, prev), start, count, d, cap=count, threads=threads)
         assert got.tolist() == want.tolist(), (k, start, count, d)
+
+
+def test_sweep_d0_full_window_count():
+    """At difficulty 0 every counter solves: a full 2^32 window has exactly
+    2^32 solutions, which the 64-bit solution count (PowResult::count) holds
+    (a 32-bit one wrapped to 0 here).  Count-only form, no list."""
+    with GpuMiner(0) as m:
+        b = make_block(1, 0, 9, 1700000000, b"")
+        n, mn = m.sweep_count(b, 0, 1 << 32, 0)
+        assert n == 1 << 32 and mn == 0
+        n, mn = m.sweep_count(b, 1000, (1 << 32) - 5, 0)
+        assert n == (1 << 32) - 5 and mn == 1000
