@@ -90,3 +90,55 @@ def test_native_group_from_torch():
             assert r is not None and r.counter == 238  # golden: first S0 solution
     finally:
         dist.destroy_process_group()
+
+
+def _board_rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), POW_GRID_PER_CU="4")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpi_blockchain_amd.miner import GpuMiner
+    from mpi_blockchain_amd.shard import ShardedMiner
+
+    out = {}
+    with GpuMiner(0) as m:
+        m.warmup()
+        sm = ShardedMiner(m, rank, world, board=True)
+        b = make_block(1, 0, 9, 1700000000, b"")
+        # lowest mode: S0's first d = 21 solution (golden) lies in rank 0's shard of
+        # the first 2^26-counter round; rank 1's shard stops on rank 0's hit
+        out["lowest"] = sm.mine(b, 0, 1 << 26, 21, round_size=1 << 26)
+        # any-mode: the first solution either rank finds; both agree on it
+        out["any"] = sm.mine(b, 0, 1 << 40, 28, any_solution=True)
+        out["any_solves"] = m.mine(b, out["any"], 1, 28) is not None if out["any"] is not None else False
+        sm.close()
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_board_two_ranks():
+    """Two processes share this GPU (gloo; RCCL would refuse two ranks on one
+    device), each a ShardedMiner rank with a named stop board: the lowest
+    counter is the golden one on both ranks, and an any-mode search ends
+    with one agreed, solving counter."""
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_board_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = dict(q.get(timeout=180) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert out[0]["lowest"] == out[1]["lowest"] == 2392323
+    assert out[0]["any"] == out[1]["any"] is not None
+    assert out[0]["any_solves"] and out[1]["any_solves"]
