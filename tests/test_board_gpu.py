@@ -142,7 +142,7 @@ def test_board_shared_between_processes():
         res = json.loads(out.strip().splitlines()[-1])
         print("peer process:", res)
         assert res["found"] is False
-        assert res["secs"] < 0.3 + 0.2, res  # not the seconds its range would take
+        assert res["secs"] < 0.3 + 0.5, res  # not the seconds its 2^34-counter range would take
         assert res["hashes"] < 1 << 33
         A.bind_board(None)
 

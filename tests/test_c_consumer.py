@@ -63,3 +63,29 @@ def test_group_example_mines(mpi_exe, tmp_path):
                        capture_output=True, text=True, cwd=tmp_path, env=mpi_env())
     assert p.returncode == 0, p.stdout + p.stderr
     assert "counter 2392323 " in p.stdout and "agreed and valid" in p.stdout, p.stdout
+
+
+@pytest.fixture(scope="module")
+def board_exe(tmp_path_factory):
+    from mpi_blockchain_amd.build import build
+
+    build()
+    out = str(tmp_path_factory.mktemp("cb") / "board_two_ctx")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-D_POSIX_C_SOURCE=200809L", "-I",
+                    os.path.join(ROOT, "include"), os.path.join(ROOT, "examples", "board_two_ctx.c"), "-L", PKG,
+                    "-lpow_gpu", f"-Wl,-rpath,{PKG}", "-lpthread", "-o", out], check=True)
+    return out
+
+
+def test_board_example_builds(board_exe):
+    assert os.path.exists(board_exe)
+
+
+@pytest.mark.gpu
+def test_board_example_stops_peer(board_exe):
+    """Two contexts, two host threads, one private stop board, from C: the
+    running context stops within 5 ms of the finder's return."""
+    p = subprocess.run([board_exe], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, POW_GRID_PER_CU="4"))
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "A: rc 1 " in p.stdout and "B: rc 0 " in p.stdout, p.stdout

@@ -7,7 +7,9 @@
 #
 #   tools/host_sanitize.sh build     # here (CPU): builds into build/san/
 #   tools/host_sanitize.sh run       # on the GPU box: runs the consumers
-#   tools/host_sanitize.sh tsan-build / tsan-run   # ThreadSanitizer on pow_node
+#   tools/host_sanitize.sh tsan-build / tsan-run   # ThreadSanitizer: pow_node and the
+#                                                   # two-context board example, with the
+#                                                   # library's host code instrumented too
 set -eu
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/build/san"
@@ -25,10 +27,12 @@ build)
     -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
     -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer \
     -I "$R/include" -I "$C" \
-    "$C/pow_api.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" "$C/valu_peak.hip" \
-    -o "$O/libpow_gpu.so"
+    "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
+    "$C/valu_peak.hip" -o "$O/libpow_gpu.so"
   $CLANG -std=c11 -O1 -g $SAN -I "$R/include" "$R/examples/mine_chain.c" \
     -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/mine_chain"
+  $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g $SAN -pthread -I "$R/include" "$R/examples/board_two_ctx.c" \
+    -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/board_two_ctx"
   $CLANGXX -std=c++17 -O1 -g $SAN -pthread -I "$R/include" -I "$MPI_INC" \
     "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' \
     "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$O/pow_node"
@@ -40,6 +44,7 @@ run)
   export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
   export LD_LIBRARY_PATH="$O${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}"
   "$O/mine_chain" 10 12
+  POW_GRID_PER_CU=4 "$O/board_two_ctx"
   W=$(mktemp -d)
   cd "$W"
   export LD_LIBRARY_PATH="/lib/x86_64-linux-gnu:$MPI_LIB:$LD_LIBRARY_PATH"
@@ -49,8 +54,8 @@ run)
   /opt/conda/bin/mpiexec -np 4 "$O/pow_node" --difficulty 9 --serial-init 1
   echo "chains d=9:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   rm -f ./*.out
-  /opt/conda/bin/mpiexec -np 6 "$O/pow_node" --difficulty 5 --serial-init 1 --winner-pause-us 400 --pause-us 200 \
-    > net_d5.log
+  /opt/conda/bin/mpiexec -np 6 "$O/pow_node" --difficulty 5 --serial-init 1 --hold-first 1 \
+    --winner-pause-us 400 --pause-us 200 > net_d5.log
   cat net_d5.log
   echo "chains d=5:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   echo "protocol paths taken (lost races, branch conflicts, chain requests):"
@@ -58,25 +63,39 @@ run)
   ;;
 tsan-build)
   # ThreadSanitizer on pow_node's own code (receive thread, miner thread, GPU
-  # set-up thread); the library and the runtimes below it are not instrumented.
-  mkdir -p "$O"
+  # set-up thread) AND on the library's host code (-Xarch_host: the cancel
+  # word, pow_cancel's epoch, the stop board's slots cross threads there);
+  # device code and the HIP/HSA/MPI runtimes below are not instrumented.
+  T="$O/tsan"
+  mkdir -p "$T"
+  C="$R/mpi_blockchain_amd/csrc"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -fPIC -shared -std=c++17 -mcode-object-version=5 \
+    -Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer -I "$R/include" -I "$C" \
+    "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
+    "$C/valu_peak.hip" -o "$T/libpow_gpu.so"
   $CLANGXX -std=c++17 -O1 -g -fsanitize=thread -pthread -I "$R/include" -I "$MPI_INC" \
-    "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$R/mpi_blockchain_amd" -lpow_gpu \
-    -Wl,-rpath,"$R/mpi_blockchain_amd" "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$O/pow_node_tsan"
-  echo "built $O/pow_node_tsan"
+    "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$T" -lpow_gpu \
+    -Wl,-rpath,'$ORIGIN' "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$T/pow_node_tsan"
+  $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g -fsanitize=thread -pthread -I "$R/include" \
+    "$R/examples/board_two_ctx.c" -L "$T" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$T/board_two_ctx_tsan"
+  echo "built $T"
   ;;
 tsan-run)
-  S="$O/tsan.supp"
+  T="$O/tsan"
+  S="$T/tsan.supp"
+  # Only the runtimes below the library are suppressed; libpow_gpu.so itself is instrumented.
   printf '%s\n' "called_from_lib:libamdhip64.so" "called_from_lib:libhsa-runtime64.so" \
-    "called_from_lib:libmpi.so" "called_from_lib:libpow_gpu.so" > "$S"
+    "called_from_lib:libmpi.so" > "$S"
   export TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1:suppressions=$S"
   export LD_LIBRARY_PATH="/lib/x86_64-linux-gnu:$MPI_LIB${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}"
+  POW_GRID_PER_CU=4 "$T/board_two_ctx_tsan"
   W=$(mktemp -d)
   cd "$W"
-  /opt/conda/bin/mpiexec -np 4 "$O/pow_node_tsan" --difficulty 9
+  /opt/conda/bin/mpiexec -np 4 "$T/pow_node_tsan" --difficulty 9
   echo "chains d=9:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   rm -f ./*.out
-  /opt/conda/bin/mpiexec -np 6 "$O/pow_node_tsan" --difficulty 5 --winner-pause-us 400 --pause-us 200 > net_d5.log
+  /opt/conda/bin/mpiexec -np 6 "$T/pow_node_tsan" --difficulty 5 --hold-first 1 --winner-pause-us 400 \
+    --pause-us 200 > net_d5.log
   cat net_d5.log
   echo "chains d=5:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   echo "protocol paths taken (lost races, branch conflicts, chain requests):"
