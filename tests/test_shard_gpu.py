@@ -142,3 +142,35 @@ def test_sharded_board_two_ranks():
     assert out[0]["lowest"] == out[1]["lowest"] == 2392323
     assert out[0]["any"] == out[1]["any"] is not None
     assert out[0]["any_solves"] and out[1]["any_solves"]
+
+
+def test_native_group_beside_torch_rccl():
+    """bench.py at N > 1 runs torch's nccl (RCCL) process group and the
+    library's own RCCL communicator (pow_group, RCCL dlopen'ed) in one
+    process: both on this GPU at world size 1, collectives on each, then a
+    group search."""
+    import torch
+    import torch.distributed as dist
+
+    from mpi_blockchain_amd.miner import GpuMiner
+    from mpi_blockchain_amd.shard import RcclGroup
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        t = torch.ones(4, device="cuda:0")
+        dist.all_reduce(t)
+        assert t.sum().item() == 4
+        with GpuMiner(0) as m, RcclGroup.from_torch(m) as g:
+            assert g.allreduce([9, 2], "min") == [9, 2]
+            r = g.mine(make_block(1, 0, 9, 1700000000, b""), 0, 1 << 20, 9)
+            assert r is not None and r.counter == 238
+            dist.all_reduce(t)  # torch's communicator still works beside ours
+            assert t.sum().item() == 4
+    finally:
+        dist.destroy_process_group()
