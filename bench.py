@@ -227,6 +227,44 @@ def protocol_runs() -> dict:
     return out
 
 
+FORK_EVENTS = ("Perdí la carrera", "Conflicto suave", "Conflicto de branch", "TAG_CHAIN_HASH")
+
+
+def protocol_job(world: int, timeout: float = 90) -> dict:
+    """BASELINE config 5 at the job's size: `mpiexec -np N pow_node`, one MPI
+    rank per GPU of this node (pow_node binds node-local rank r to GPU r), the
+    reference's protocol (broadcast, validation, chain migration) with GPU
+    mining, 10 blocks.  Run by rank 0 after the timed region while the other
+    bench ranks wait idle.  d = 9 (the reference's DEFAULT_DIFFICULTY), d = 25
+    (real mining: 10 x 2^25 expected trials) and d = 5 with a forced fork
+    (--hold-first: every rank mines its own block 1, published after a
+    barrier, so every rank must resolve rival blocks)."""
+    import re
+    import tempfile
+
+    from mpi_blockchain_amd.build import mpi_available
+    from mpi_blockchain_amd.node import chain_status, run_network
+
+    if not mpi_available():
+        return {"skipped": "no MPI"}
+    out = {"ranks": world, "blocks": 10}
+    for key, d, extra in (("d9", 9, ()), ("d25", 25, ()), ("d5_forced_fork", 5, ("--hold-first", "1"))):
+        try:
+            with tempfile.TemporaryDirectory() as td:
+                t = time.perf_counter()
+                run = run_network(world, td, difficulty=d, blocks=10, timeout=timeout, extra_args=extra)
+                wall = time.perf_counter() - t
+            st = [chain_status(c, 10, d) for c in run.chains.values()]
+            out[key] = {"wall_s": round(wall, 3), "rc": run.returncode,
+                        "chains_consistent": all(ok for ok, _ in st), "chains_complete": sum(c for _, c in st),
+                        "blocks_mined": len(re.findall(r"Agregué un producido", run.stdout)),
+                        "fork_events": sum(run.stdout.count(m) for m in FORK_EVENTS),
+                        "hard_errors": run.stdout.count("Error duro")}
+        except Exception as e:  # pragma: no cover - reported, not fatal
+            out[key] = {"error": str(e)[-300:]}
+    return out
+
+
 def ladder(miner, n_templates: int = 101, rungs=(9, 13, 17, 21, 25)) -> dict:
     """BASELINE config 3: time-to-block (median over templates, seed 1) and
     sustained hashes/s per difficulty rung.  Time-to-block uses pow_mine_any
@@ -327,6 +365,7 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        idle_group = dist.new_group(backend="gloo")  # host-side waits (protocol_job)
 
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
     from mpi_blockchain_amd.shard import RcclGroup
@@ -343,6 +382,15 @@ def main():
         except Exception as e:  # pragma: no cover - fall back to torch's collectives, say so
             group_err = f"pow_group_init failed ({e}); torch.distributed collectives used instead"
             group = None
+        if dist is not None:
+            # Every rank uses the native group or none does (a rank that lacks it
+            # would leave its peers waiting in the group's collectives).
+            ok = torch.tensor([1 if group is not None else 0], dtype=torch.int64, device=f"cuda:{local}")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and group is not None:
+                group.close()
+                group = None
+                group_err = "pow_group_init failed on a peer rank; torch.distributed collectives used instead"
     info = miner.device_info()
     tmpl = s0_block()
     d = args.difficulty
@@ -404,6 +452,13 @@ def main():
             gsearch = group_search(group, rank, world)
         except Exception as e:  # pragma: no cover - reported, not fatal: the headline is measured
             gsearch = {"error": str(e)[-300:]}
+    # Config 5 on this job's GPUs (rank 0 launches the MPI job; the other
+    # ranks wait on a gloo barrier, which keeps no kernel on their GPUs).
+    proto = None
+    if dist is not None and world > 1 and not args.no_protocol:
+        if rank == 0:
+            proto = protocol_job(world)
+        dist.barrier(group=idle_group)
     if rank != 0:
         buf.free()
         if group is not None:
@@ -479,6 +534,8 @@ def main():
         res["group_error"] = group_err
     if world == 1 and not args.no_protocol:
         res["protocol"] = protocol_runs()
+    if proto is not None:
+        res["protocol"] = proto
     buf.free()
     if group is not None:
         group.close()

@@ -33,8 +33,16 @@ class NetworkRun:
     chains: dict = field(default_factory=dict)  # rank -> [ChainEntry] (tip first)
 
 
+# A launcher's rank variables (torch.distributed.run sets these in bench.py's
+# ranks) must not reach MPI jobs started from such a rank: pow_node takes its
+# node-local rank from the MPI launcher's own variables.
+_FOREIGN_RANK_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                      "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
 def mpi_env() -> dict:
-    env = dict(os.environ)
+    env = {k: v for k, v in os.environ.items()
+           if k not in _FOREIGN_RANK_VARS and not k.startswith("TORCHELASTIC_")}
     # MPICH's lib dir also holds an old libstdc++: keep the system one first.
     env["LD_LIBRARY_PATH"] = ":".join(
         p for p in ("/lib/x86_64-linux-gnu", os.path.join(MPI_HOME, "lib"), env.get("LD_LIBRARY_PATH", "")) if p)
@@ -49,6 +57,18 @@ def parse_chain_dump(text: str) -> list[ChainEntry]:
                          r"Block hash: ([^\n]*)\n", text):
         out.append(ChainEntry(int(m.group(1)), int(m.group(2)), m.group(3), m.group(4)))
     return out
+
+
+def chain_status(entries: list[ChainEntry], blocks: int, difficulty: int) -> tuple[bool, bool]:
+    """(consistent, complete) for a logged chain, tip first: consecutive
+    indices, each block linked to the next one's hash, every hash solving
+    `difficulty` leading zero bits; complete = blocks..1 down to genesis."""
+    idx = [e.index for e in entries]
+    ok = idx == list(range(idx[0], idx[0] - len(idx), -1)) if idx else True
+    ok = ok and all(cur.prev == prev.hash for cur, prev in zip(entries, entries[1:]))
+    ok = ok and all(len(e.hash) == 64 and re.fullmatch(r"[0-9a-f]{64}", e.hash) is not None
+                    and 256 - int(e.hash, 16).bit_length() >= difficulty for e in entries)
+    return ok, ok and idx == list(range(blocks, 0, -1)) and entries[-1].prev == ""
 
 
 def run_network(n_gpu: int, workdir: str, difficulty: int = 9, blocks: int = 10, timeout: float = 240,

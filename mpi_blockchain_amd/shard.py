@@ -111,8 +111,17 @@ class RcclGroup:
         rank 0 makes the id, every rank receives it, all join."""
         import torch.distributed as dist
 
-        obj = [cls.make_unique_id() if dist.get_rank(group) == 0 else None]
+        # Rank 0 always broadcasts (its error text if it could not make an id),
+        # so no peer is left waiting in the broadcast or in ncclCommInitRank.
+        obj = [None]
+        if dist.get_rank(group) == 0:
+            try:
+                obj[0] = cls.make_unique_id()
+            except Exception as e:
+                obj[0] = f"rank 0: {e}"
         dist.broadcast_object_list(obj, src=0, group=group)
+        if isinstance(obj[0], str):
+            raise RuntimeError(obj[0])
         return cls(miner, dist.get_rank(group), dist.get_world_size(group), obj[0])
 
     def allreduce(self, vals, op: str = "min") -> list[int]:

@@ -53,6 +53,13 @@ def run_rehearsal(n: int) -> dict:
     assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 1e9
     assert "gloo all_reduce" in d["config"]["parallelism"]
     assert "cpu_baseline" not in d and "ladder" not in d  # rank-0-at-N=1-only extras
+    # config 5 at the job's size: mpiexec -np n pow_node (here all on the one GPU)
+    pr = d["protocol"]
+    assert pr["ranks"] == n
+    for key in ("d9", "d25", "d5_forced_fork"):
+        assert pr[key]["rc"] == 0 and pr[key]["chains_consistent"] and pr[key]["chains_complete"] >= 1, pr
+        assert pr[key]["hard_errors"] == 0, pr
+    assert pr["d5_forced_fork"]["blocks_mined"] >= n and pr["d5_forced_fork"]["fork_events"] >= 1, pr
     return d
 
 

@@ -47,10 +47,13 @@ def half_grid_miner():
 
 @pytest.mark.parametrize("any_solution", [True, False])
 def test_board_stops_running_peer(any_solution):
-    """Context B mines a range with no solution (d = 64, 2^32 counters:
-    ~1 s); context A then finds S0's first d = 9 solution and its kernel
-    publishes it.  B must stop within a few ms of A's return, in both modes
-    (lowest mode: A's counter 238 is below every counter B would compute)."""
+    """Context B mines a range with no solution (d = 64, 2^34 counters:
+    ~2 s even at the whole GPU's rate); context A then finds S0's first d = 9
+    solution and its kernel publishes it.  B must stop within a few ms of A's
+    return, in both modes (lowest mode: A's counter 238 is below every counter
+    B would compute).  B's half grid still runs near the full rate while A is
+    idle, and A's call itself takes 20-110 ms beside B, so the check is on
+    B's stop time, not on a trial count tied to the sleep below."""
     from mpi_blockchain_amd.miner import GpuMiner, StopBoard
 
     b = s0()
@@ -62,7 +65,7 @@ def test_board_stops_running_peer(any_solution):
 
         def run_b():
             t = time.perf_counter()
-            res["r"] = B.mine(b, 1 << 33, 1 << 32, 64, any_solution=any_solution)
+            res["r"] = B.mine(b, 1 << 36, 1 << 34, 64, any_solution=any_solution)
             res["end"] = time.perf_counter()
             res["secs"] = res["end"] - t
             res["hashes"] = B.stats()["hashes"]
@@ -83,8 +86,8 @@ def test_board_stops_running_peer(any_solution):
         lag = res["end"] - a_end
         print(f"any={any_solution}: B stopped {1e3 * lag:.3f} ms after A returned; "
               f"B ran {res['secs']:.3f} s, {res['hashes']} trials")
-        assert lag < 0.005, lag
-        assert res["hashes"] < (1 << 32) // 2
+        assert -0.001 < lag < 0.005, lag  # B was still running when A returned, and stopped at once
+        assert res["hashes"] < (1 << 34) // 2
         A.bind_board(None)
         B.bind_board(None)
 
