@@ -72,6 +72,24 @@ __device__ __forceinline__ void const_chunk(St& t, cptr kwbase, uint32_t dep) {
   }
 }
 
+// K1's form of const_chunk: the K+W words come from LDS (a per-workgroup copy
+// of C->kw) into VGPRs, 4 per ds_read_b128 (every lane reads the same address:
+// a broadcast), so the K+W add has two VGPR operands.  A VALU op with an SGPR
+// operand issues at half rate on gfx950; moving these 256 adds
+// per trial off SGPRs made the sweep 0.7% faster (profiles/r02/ab/).  Chunk
+// 0's K and K+W words stay scalar loads: its SGPR operands sit in v_add3
+// (half rate anyway), and LDS copies of them measured 0.4-0.6% slower.
+__device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
+#pragma unroll
+  for (int g = 0; g < 64; g += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
+    round_kw(t, v.x);
+    round_kw(t, v.y);
+    round_kw(t, v.z);
+    round_kw(t, v.w);
+  }
+}
+
 // Append the 32-entry-aligned part of a wave's staged solutions (nst <= 127,
 // in LDS) to the global list with one atomic; the remainder (< 32) moves to
 // the stage front.  Every reservation is a multiple of 32 entries, so each
@@ -207,6 +225,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
   uint32_t* wst = stage[threadIdx.x >> 6];
   uint32_t nst = 0;                     // staged entries (wave-uniform)
   unsigned long long mymin = ~0ull;     // lowest solution of this lane
+  // chunks 1-4's K+W words, one per thread (blockDim = 256 = 4 x 64)
+  __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
+  lkw[threadIdx.x] = (&C->kw[0][0])[threadIdx.x];
+  __syncthreads();
 
   for (;;) {
     uint32_t got = 0;
@@ -344,13 +366,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-        const_chunk(t, as_const(C->kw[c]), H[0]);
+        const_chunk_lds(t, lkw + 64 * c);
         H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
         H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
       }
       // ---------------- chunk 4 (last): only what the test needs ----------------
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk(t, as_const(C->kw[3]), H[0]);
+      const_chunk_lds(t, lkw + 64 * 3);
       const uint32_t h0 = H[0] + t.a;
 
       bool hit = h0 <= L.thr;

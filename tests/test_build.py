@@ -77,17 +77,22 @@ def test_no_spills_and_occupancy(isa, variant):
 @pytest.mark.parametrize("variant", ["_Z10pow_searchILi0ELb0E", "_Z10pow_searchILi1ELb0E"])
 def test_j_loop_clean(isa, variant):
     body = j_loop_body(isa, variant)
-    ops = re.findall(r"^\s+([sv]_[a-z0-9_]+|flat_\w+|global_\w+|scratch_\w+|buffer_\w+)", body, flags=re.M)
+    ops = re.findall(r"^\s+([sv]_[a-z0-9_]+|ds_\w+|flat_\w+|global_\w+|scratch_\w+|buffer_\w+)", body, flags=re.M)
     valu = [o for o in ops if o.startswith("v_")]
     # one trial: chunk-0 rounds 3..63 + schedule, chunks 1-4, test ~= 4,850 VALU
     assert 4700 <= len(valu) <= 5000, len(valu)
     assert "v_readlane_b32" not in ops and "v_writelane_b32" not in ops
     assert not [o for o in ops if o.startswith(("flat_", "global_", "scratch_", "buffer_"))], \
-        "the j-loop must take its constants through scalar loads only"
-    # the 4 x 64 template K+W words (and K[16..63]) arrive by scalar loads
+        "the j-loop must take its constants through scalar and LDS loads only"
+    # chunk 0's uniform words (K[16..63], K+W[4..15], the j terms) arrive by
+    # scalar loads; chunks 1-4's 4 x 64 K+W words by LDS broadcast reads into
+    # VGPRs (no SGPR operand in their K+W adds)
     words = sum({"s_load_dwordx16": 16, "s_load_dwordx8": 8, "s_load_dwordx4": 4, "s_load_dwordx2": 2,
                  "s_load_dword": 1}.get(o, 0) for o in ops)
-    assert words >= 256, words
+    assert words >= 48 + 12, words
+    assert ops.count("ds_read_b128") == 64, ops.count("ds_read_b128")
+    sgpr_adds = len(re.findall(r"^\s+v_add_u32_e32 [^\n]*\bs\d+", body, flags=re.M))
+    assert sgpr_adds <= 16, sgpr_adds
 
 
 def test_k2_fits_beside_k1(isa):
