@@ -227,6 +227,24 @@ def protocol_runs() -> dict:
     return out
 
 
+def wait_for_exit(pids, timeout: float) -> bool:
+    """True once none of `pids` (this node's other bench ranks) is alive
+    (a zombie waiting for the launcher to reap it holds no GPU)."""
+    t = time.time()
+    while time.time() - t < timeout:
+        alive = 0
+        for pid in pids:
+            try:
+                with open(f"/proc/{pid}/stat") as f:
+                    alive += f.read().rsplit(")", 1)[1].split()[0] != "Z"
+            except OSError:
+                pass
+        if not alive:
+            return True
+        time.sleep(0.05)
+    return False
+
+
 FORK_EVENTS = ("Perdí la carrera", "Conflicto suave", "Conflicto de branch", "TAG_CHAIN_HASH")
 
 
@@ -365,7 +383,6 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        idle_group = dist.new_group(backend="gloo")  # host-side waits (protocol_job)
 
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
     from mpi_blockchain_amd.shard import RcclGroup
@@ -452,19 +469,24 @@ def main():
             gsearch = group_search(group, rank, world)
         except Exception as e:  # pragma: no cover - reported, not fatal: the headline is measured
             gsearch = {"error": str(e)[-300:]}
-    # Config 5 on this job's GPUs (rank 0 launches the MPI job; the other
-    # ranks wait on a gloo barrier, which keeps no kernel on their GPUs).
+    # Config 5 on this job's GPUs: rank 0 launches the MPI job once every
+    # other bench rank has exited (their processes release the GPUs, so each
+    # GPU carries one pow_node rank and at most bench rank 0 besides).
     proto = None
-    if dist is not None and world > 1 and not args.no_protocol:
-        if rank == 0:
-            proto = protocol_job(world)
-        dist.barrier(group=idle_group)
+    do_proto = dist is not None and world > 1 and not args.no_protocol
+    pids = None
+    if do_proto:
+        pids = [None] * world
+        dist.all_gather_object(pids, os.getpid())
     if rank != 0:
         buf.free()
         if group is not None:
             group.close()
         dist.destroy_process_group()
         return
+    if do_proto:
+        gone = wait_for_exit(pids[1:], timeout=120)
+        proto = protocol_job(world) if gone else {"skipped": "bench ranks 1..N-1 did not exit within 120 s"}
     collective = ("rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if group is not None and world > 1
                   else f"{dist.get_backend()} all_reduce(min,sum) per step via torch.distributed" if dist is not None
                   else "none (single process)")

@@ -83,10 +83,10 @@ __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
 #pragma unroll
   for (int g = 0; g < 64; g += 4) {
     const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
-    round_kw(t, v.x);
-    round_kw(t, v.y);
-    round_kw(t, v.z);
-    round_kw(t, v.w);
+    round_kw_o(t, v.x);
+    round_kw_o(t, v.y);
+    round_kw_o(t, v.z);
+    round_kw_o(t, v.w);
   }
 }
 
@@ -316,48 +316,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       cptr J = pin(Cb, s2.a ^ j);  // per-j words and the chunk-0 uniform terms
       const uint32_t kw3 = J[PC_KW3 + j];
       St s{A3 + kw3, s2.a, s2.b, s2.c, E3 + kw3, s2.e, s2.f, s2.g};
+      // Every round in round_ordered's issue order (sha256_dev.h); each
+      // schedule word is computed just before its round (computing it one
+      // round earlier measured 0.9% slower, profiles/r02/ab/ab8).
 #pragma unroll
-      for (int i = 4; i < 16; ++i) round_kw(s, J[PC_KW0 + i]);
-      cptr Kp = pin(Cb + PC_K, s.e);  // K[16..63], streamed like the K+W words
+      for (int i = 4; i < 16; ++i) round_kw_o(s, J[PC_KW0 + i]);
       uint32_t w[64];
       w[16] = W16;
       w[17] = W17;
-      round_k_w(s, Kp[16], W16);
-      round_k_w(s, Kp[17], W17);
-      w[18] = c18 + J[PC_U18 + j];
-      round_k_w(s, Kp[18], w[18]);
-      w[19] = c19 + J[PC_W3 + j];
-      round_k_w(s, Kp[19], w[19]);
-      w[20] = ssig1(w[18]) + J[PC_U20];
-      round_k_w(s, Kp[20], w[20]);
-      w[21] = ssig1(w[19]) + J[PC_U20 + 1];
-      round_k_w(s, Kp[21], w[21]);
-      w[22] = ssig1(w[20]) + J[PC_U20 + 2];
-      round_k_w(s, Kp[22], w[22]);
-      w[23] = ssig1(w[21]) + c23;
-      round_k_w(s, Kp[23], w[23]);
-      w[24] = ssig1(w[22]) + c24;
-      round_k_w(s, Kp[24], w[24]);
+      // schedule word i (template-uniform and per-prefix terms folded)
+      auto wcalc = [&](int i) {
+        if (i == 18) w[18] = c18 + J[PC_U18 + j];
+        else if (i == 19) w[19] = c19 + J[PC_W3 + j];
+        else if (i <= 22) w[i] = ssig1(w[i - 2]) + J[PC_U20 + i - 20];
+        else if (i == 23) w[23] = ssig1(w[21]) + c23;
+        else if (i == 24) w[24] = ssig1(w[22]) + c24;
+        else if (i <= 30) w[i] = ssig1(w[i - 2]) + w[i - 7] + J[PC_U25 + i - 25];
+        else if (i == 31) w[31] = ssig1(w[29]) + w[24] + c31;
+        else if (i == 32) w[32] = ssig1(w[30]) + w[25] + c32;
+        else w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
+      };
+      auto rnd = [&](int i, cptr Kx) {
+        if (i >= 18) wcalc(i);
+        round_k_w_o(s, Kx[i], w[i]);
+      };
+      {
+        cptr Kp = pin(Cb + PC_K, s.e);  // K[16..63], streamed like the K+W words
 #pragma unroll
-      for (int i = 25; i < 31; ++i) {
-        w[i] = ssig1(w[i - 2]) + w[i - 7] + J[PC_U25 + i - 25];
-        round_k_w(s, Kp[i], w[i]);
+        for (int i = 16; i < 32; ++i) rnd(i, Kp);
       }
-      w[31] = ssig1(w[29]) + w[24] + c31;
-      round_k_w(s, Kp[31], w[31]);
-      cptr K2 = pin(Cb + PC_K, s.e);
-      w[32] = ssig1(w[30]) + w[25] + c32;
-      round_k_w(s, K2[32], w[32]);
+      {
+        cptr K2 = pin(Cb + PC_K, s.e);
 #pragma unroll
-      for (int i = 33; i < 48; ++i) {
-        w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
-        round_k_w(s, K2[i], w[i]);
+        for (int i = 32; i < 48; ++i) rnd(i, K2);
       }
-      cptr K3 = pin(Cb + PC_K, s.e);
+      {
+        cptr K3 = pin(Cb + PC_K, s.e);
 #pragma unroll
-      for (int i = 48; i < 64; ++i) {
-        w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
-        round_k_w(s, K3[i], w[i]);
+        for (int i = 48; i < 64; ++i) rnd(i, K3);
       }
       uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
                        IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};
