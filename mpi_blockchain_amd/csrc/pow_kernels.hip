@@ -15,7 +15,7 @@
 //   * the lane loops over j = 0..61 (the last nonce char, word W3) — j is
 //     wave-uniform, so W3 and every term derived from it are scalar loads.
 //   Per trial the lane runs chunk-0 rounds 4..63 and chunks 1-4 (whose K+W
-//   come from SGPRs: template-constant schedule) — no memory traffic.
+//   are template constants, read from an LDS copy) — no memory traffic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -55,25 +55,8 @@ __device__ __forceinline__ cptr pin(cptr p, uint32_t dep) {
   return p;
 }
 
-// 64 rounds of a chunk whose K+W are template constants, streamed through
-// SGPRs in groups of 16: group g+1's scalar loads are pinned behind the state
-// of round 16g+8, so at most two groups (32 SGPRs) are live and each group's
-// loads have 8 rounds to land.  (All 64 at once needs > 80 SGPRs, which cuts
-// residency from 8 to 6 workgroups per CU.)
-__device__ __forceinline__ void const_chunk(St& t, cptr kwbase, uint32_t dep) {
-#pragma unroll
-  for (int g = 0; g < 64; g += 16) {
-    cptr kw = pin(kwbase + g, dep);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      round_kw(t, kw[i]);
-      if (i == 7) dep = t.e;
-    }
-  }
-}
-
-// K1's form of const_chunk: the K+W words come from LDS (a per-workgroup copy
-// of C->kw) into VGPRs, 4 per ds_read_b128 (every lane reads the same address:
+// 64 rounds of a chunk whose K+W are template constants (chunks 1-4, K1 and
+// K1'): the K+W words come from LDS (a per-workgroup copy of C->kw) into VGPRs, 4 per ds_read_b128 (every lane reads the same address:
 // a broadcast), so the K+W add has two VGPR operands.  A VALU op with an SGPR
 // operand issues at half rate on gfx950; moving these 256 adds
 // per trial off SGPRs made the sweep 0.7% faster (profiles/r02/ab/).  Chunk
@@ -475,6 +458,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   bool wrote_hit = false;  // this wave wrote a hit record (wave-uniform after each step)
   __shared__ uint32_t wg_iters;  // wave-iterations of this workgroup
   if (threadIdx.x == 0) wg_iters = 0;
+  // chunks 1-4's K+W words (PowConsts::kw), one per thread, as in K1
+  __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
+  lkw[threadIdx.x] = Cb[threadIdx.x];
   __syncthreads();
   for (unsigned long long qq = (unsigned long long)wave * 64u; qq < L.count;
        qq += (unsigned long long)nwaves * 64u) {
@@ -507,34 +493,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     w[3] |= digit_char(dg[8]) << 24;  // [nonce[8], NUL, prev0, prev1]
     St s{P[PC_ST0 + 0], P[PC_ST0 + 1], P[PC_ST0 + 2], P[PC_ST0 + 3],
          P[PC_ST0 + 4], P[PC_ST0 + 5], P[PC_ST0 + 6], P[PC_ST0 + 7]};  // after round 0
-    round_k_w(s, P[PC_K + 1], w[1]);
-    round_k_w(s, P[PC_K + 2], w[2]);
-    round_k_w(s, P[PC_K + 3], w[3]);
+    round_k_w_o(s, P[PC_K + 1], w[1]);
+    round_k_w_o(s, P[PC_K + 2], w[2]);
+    round_k_w_o(s, P[PC_K + 3], w[3]);
 #pragma unroll
-    for (int i = 4; i < 16; ++i) round_kw(s, P[PC_KW0 + i]);
+    for (int i = 4; i < 16; ++i) round_kw_o(s, P[PC_KW0 + i]);
     cptr Kp = pin(Cb + PC_K, s.e);
 #pragma unroll
     for (int i = 16; i < 40; ++i) {
       w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
-      round_k_w(s, Kp[i], w[i]);
+      round_k_w_o(s, Kp[i], w[i]);
     }
     cptr K2 = pin(Cb + PC_K, s.e);
 #pragma unroll
     for (int i = 40; i < 64; ++i) {
       w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
-      round_k_w(s, K2[i], w[i]);
+      round_k_w_o(s, K2[i], w[i]);
     }
     uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
                      IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};
+    // an opaque offset (always 0) keeps the 256 LDS reads inside the loop:
+    // hoisted out of it, they would take 256 VGPRs
+    uint32_t lo = 0;
+    asm volatile("" : "+v"(lo) : "v"(s.a));
+    const uint32_t* lk = lkw + lo;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk(t, Cb + 64 * c, H[0]);  // PowConsts::kw[c]
+      const_chunk_lds(t, lk + 64 * c);
       H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
       H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
     }
     St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-    const_chunk(t, Cb + 64 * 3, H[0]);
+    const_chunk_lds(t, lk + 64 * 3);
     // The whole digest stays live here (this kernel runs at <= 4 waves/SIMD,
     // so the 7 extra VGPRs cost no residency): a hit records it, and the
     // winner's block_hash needs no K2 launch (one serial SHA-256 of 5 chunks

@@ -52,13 +52,6 @@ struct St {
   uint32_t a, b, c, d, e, f, g, h;
 };
 
-// One round whose K[i]+W[i] is a single (usually wave-uniform, SGPR) value.
-__device__ __forceinline__ void round_kw(St& s, uint32_t kw) {
-  uint32_t t1 = s.h + bsig1(s.e) + ch(s.e, s.f, s.g) + kw;
-  uint32_t t2 = bsig0(s.a) + maj(s.a, s.b, s.c);
-  s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
-  s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
-}
 // One round with separate K (uniform) and W (per lane): add3(h,S1,Ch), add3(.,K,W).
 __device__ __forceinline__ void round_k_w(St& s, uint32_t k, uint32_t w) {
   uint32_t t1 = s.h + bsig1(s.e) + ch(s.e, s.f, s.g) + k + w;

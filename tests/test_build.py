@@ -110,3 +110,9 @@ def test_latency_kernel_no_private_copy(isa, variant):
     pointer; taking the parameter's address would copy 2.3 KB to scratch."""
     md = metadata(isa, variant)
     assert md["private_segment_fixed_size"] == 0 and md["vgpr_spill_count"] == 0, md
+    # it runs at <= 4 waves per SIMD (pow_api.cpp run_search_lat): <= 128 VGPRs
+    assert md["vgpr_count"] <= 128, md
+    # chunks 1-4's K+W come from the LDS copy inside the loop, as in K1 (hoisted
+    # out of it, the 256 words would take 256 VGPRs)
+    body = j_loop_body(isa, variant)
+    assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 64
