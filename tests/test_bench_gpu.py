@@ -29,6 +29,11 @@ def test_bench_json_contract():
     assert r["bound"] and r["peak"] > 0 and 0 < r["frac"] < 1.5
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert d["parity"]["count_ok"] is True
+    # traffic measured in the run (two rocprofv3 PMC passes): at least the
+    # solution list (4 B per solution), at most a few times it
+    assert "total_bytes" in r["traffic_live"], r["traffic_live"]
+    assert r["traffic"] == r["traffic_live"]["total_bytes"] and "measured in this run" in r["traffic_source"]
+    assert r["algorithmic_bytes"] <= r["traffic"] < 4 * r["algorithmic_bytes"], r
 
 
 def run_rehearsal(n: int) -> dict:

@@ -79,8 +79,9 @@ def test_j_loop_clean(isa, variant):
     body = j_loop_body(isa, variant)
     ops = re.findall(r"^\s+([sv]_[a-z0-9_]+|ds_\w+|flat_\w+|global_\w+|scratch_\w+|buffer_\w+)", body, flags=re.M)
     valu = [o for o in ops if o.startswith("v_")]
-    # one trial: chunk-0 rounds 3..63 + schedule, chunks 1-4, test ~= 4,850 VALU
-    assert 4700 <= len(valu) <= 5000, len(valu)
+    # one trial: chunk-0 rounds 4..63 + schedule, chunks 1-4, test = 4,831 VALU
+    # (PMC: 4,837 per hash with the per-chunk work, profiles/r02/final)
+    assert 4800 <= len(valu) <= 4860, len(valu)
     assert "v_readlane_b32" not in ops and "v_writelane_b32" not in ops
     assert not [o for o in ops if o.startswith(("flat_", "global_", "scratch_", "buffer_"))], \
         "the j-loop must take its constants through scalar and LDS loads only"
@@ -116,3 +117,5 @@ def test_latency_kernel_no_private_copy(isa, variant):
     # out of it, the 256 words would take 256 VGPRs)
     body = j_loop_body(isa, variant)
     assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 64
+    # one trial per lane, nothing hoisted across j: 5,083 VALU (K1: 4,831)
+    assert 5000 <= len(re.findall(r"^\s+v_", body, flags=re.M)) <= 5120

@@ -6,7 +6,7 @@ set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 tag=${1:-r01}
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 3 --warmup 1 --no-ladder --no-cpu-baseline --no-peak --no-protocol --no-group-search"
+B="$R/bench.py --steps 3 --warmup 1 --no-ladder --no-cpu-baseline --no-peak --no-protocol --no-group-search --no-pmc"
 S="$R/tools/gpu_step.sh"
 $S prof_${tag}_kt 300 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof_${tag}_kt" -o run -- python $B &&
 $S prof_${tag}_pmc1 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_WAVES -f csv --kernel-include-regex pow_search -d "$R/gpurun_out/prof_${tag}_pmc1" -o run -- python $B &&
