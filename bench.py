@@ -225,7 +225,7 @@ def protocol_runs() -> dict:
             return {"skipped": "no MPI"}
         ref = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref")
         if os.path.exists(ref):
-            with tempfile.TemporaryDirectory() as td:
+            with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
                 t = time.perf_counter()
                 p = subprocess.run(["timeout", "-k", "5", "120", MPIEXEC, "-np", "4", ref], cwd=td,
                                    env=mpi_env(), capture_output=True, text=True)
@@ -237,7 +237,7 @@ def protocol_runs() -> dict:
         # second core in MPI_Recv: 4 ranks occupy 8 CPUs.
         ref17 = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref_d17")
         if os.path.exists(ref17):
-            with tempfile.TemporaryDirectory() as td:
+            with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
                 t = time.perf_counter()
                 p = subprocess.run(["timeout", "-k", "5", "120", MPIEXEC, "-np", "4", ref17], cwd=td,
                                    env=mpi_env(), capture_output=True, text=True)
@@ -248,7 +248,7 @@ def protocol_runs() -> dict:
         else:
             out["reference_np4_d17"] = "unmeasured: oracle/_ref/blockchain_ref_d17 not built"
         for d in (9, 17, 25):
-            with tempfile.TemporaryDirectory() as td:
+            with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
                 t = time.perf_counter()
                 run = run_network(4, td, difficulty=d, blocks=10, timeout=180)
                 out[f"gpu_np4_d{d}_wall_s"] = round(time.perf_counter() - t, 3)
@@ -257,7 +257,7 @@ def protocol_runs() -> dict:
         # The reference's own published experiment closest to real mining
         # (d = 18, 3 nodes, 10 blocks, median 44.831 s on
         # unstated hardware); tools/published_replay.py replays the whole table.
-        with tempfile.TemporaryDirectory() as td:
+        with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
             t = time.perf_counter()
             run = run_network(3, td, difficulty=18, blocks=10, timeout=180)
             out["gpu_np3_d18_wall_s"] = round(time.perf_counter() - t, 3)
@@ -309,7 +309,7 @@ def protocol_job(world: int, timeout: float = 90) -> dict:
     out = {"ranks": world, "blocks": 10}
     for key, d, extra in (("d9", 9, ()), ("d25", 25, ()), ("d5_forced_fork", 5, ("--hold-first", "1"))):
         try:
-            with tempfile.TemporaryDirectory() as td:
+            with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
                 t = time.perf_counter()
                 run = run_network(world, td, difficulty=d, blocks=10, timeout=timeout, extra_args=extra)
                 wall = time.perf_counter() - t

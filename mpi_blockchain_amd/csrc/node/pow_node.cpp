@@ -39,7 +39,7 @@
 // reference.
 //
 //   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US]
-//            [--winner-pause-us US] [--serial-init 0|1] [--hold-first 0|1]
+//            [--winner-pause-us US] [--serial-init 0|1] [--hold-first 0|1] [--idle-below K]
 #include <mpi.h>
 #include <unistd.h>
 
@@ -85,6 +85,8 @@ struct Options {
                             // (and no start barrier: mixed jobs with reference ranks)
   bool hold_first = false;  // tests: every rank mines block 1, then all publish it after one
                             // MPI_Barrier, so every rank receives a rival block 1 (a certain fork)
+  unsigned idle_below = 0;  // tests: do not mine while the chain is below this index (the blocks
+                            // before it come from other ranks, e.g. the reference's CPU ranks)
 };
 
 // MPI_Probe that sleeps between polls instead of spinning.  MPICH's blocking
@@ -352,6 +354,10 @@ class Node {
         tmpl = *last_;
         ep = __atomic_load_n(&epoch_, __ATOMIC_SEQ_CST);
       }
+      if (tmpl.index < opt_.idle_below) {  // --idle-below: only receive for now
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        continue;
+      }
       // node.cpp:295-299
       tmpl.index += 1;
       tmpl.node_owner_number = (uint32_t)rank_;
@@ -496,6 +502,7 @@ int main(int argc, char** argv) {
     else if (k == "--winner-pause-us") o.winner_pause_us = (unsigned)v;
     else if (k == "--serial-init") o.serial_init = v != 0;
     else if (k == "--hold-first") o.hold_first = v != 0;
+    else if (k == "--idle-below") o.idle_below = (unsigned)std::max(0l, v);
   }
   Node n(o);
   int gpu_rc = 0;

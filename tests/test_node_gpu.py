@@ -56,8 +56,12 @@ def test_mixed_with_reference_nodes(tmp_path):
     GPU-mined blocks, the GPU ranks validate the reference's."""
     # --serial-init 1: GPU set-up before MPI_Init, so MPI_Init is every rank's
     # start line as in the reference (reference ranks join no start barrier).
+    # --idle-below 3: the GPU ranks mine only once the chain holds block 3, so blocks 1-3
+    # come from the reference ranks and both directions of adoption are
+    # certain (with a timing knob alone, a slow box let the GPU ranks win all
+    # 10 blocks in 1 of 2 runs: profiles/r02/verify/protocol_soak_mixed_*.log).
     run = run_network(2, str(tmp_path), difficulty=9, blocks=10, timeout=240, ref_binary=REF_BIN, n_ref=2,
-                      extra_args=("--pause-ms", "5", "--serial-init", "1"))
+                      extra_args=("--serial-init", "1", "--idle-below", "3"))
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout, run.stdout[-3000:]
     # reference ranks 0/1 accepted blocks sent by GPU ranks 2/3

@@ -13,7 +13,7 @@ from mpi_blockchain_amd.build import build_node  # noqa: E402
 from mpi_blockchain_amd.node import MPIEXEC, mpi_env  # noqa: E402
 
 np_, d = sys.argv[1], sys.argv[2]
-with tempfile.TemporaryDirectory() as td:
+with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
     t0 = time.perf_counter()
     p = subprocess.Popen(["timeout", "-k", "5", "120", MPIEXEC, "-np", np_, build_node(), "--difficulty", d,
                           "--blocks", "10", *sys.argv[3:]], cwd=td, env=mpi_env(), stdout=subprocess.PIPE,

@@ -47,7 +47,7 @@ def sample(cmd, secs, cwd):
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 34
-with tempfile.TemporaryDirectory() as td:
+with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
     node = os.path.abspath(sys.argv[3]) if len(sys.argv) > 3 else build_node()
     used = sample([MPIEXEC, "-np", str(n), node, "--difficulty", str(d), "--blocks", "100"], 3.0, td)
     print({"ranks": len(used), "difficulty": d, "node": node,

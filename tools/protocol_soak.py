@@ -10,6 +10,7 @@ consecutive, solving) with at least one complete 10-block chain.
 The loop stops at the first failed run (no retries): its output is printed.
 
     python tools/protocol_soak.py --runs 40 --ranks 8 --difficulty 5
+    python tools/protocol_soak.py --runs 40 --ranks 8 --difficulty 5 --forced-fork
     python tools/protocol_soak.py --runs 20 --ranks 2 --ref 2 --difficulty 9   # mixed networks
 
 With --ref K the job also holds K ranks of the REFERENCE's own binary
@@ -38,16 +39,21 @@ def main() -> int:
     ap.add_argument("--difficulty", type=int, default=5)
     ap.add_argument("--timeout", type=float, default=60)
     ap.add_argument("--ref", type=int, default=0, help="reference (CPU) ranks in the same job")
+    ap.add_argument("--forced-fork", action="store_true",
+                    help="--hold-first 1 instead of the timing knobs: every rank mines its own block 1 and "
+                         "publishes it after a barrier, so every run must show rival blocks")
     a = ap.parse_args()
-    extra = ("--winner-pause-us", "400", "--pause-us", "200")
+    extra = ("--hold-first", "1") if a.forced_fork else ("--winner-pause-us", "400", "--pause-us", "200")
     ref = dict(ref_binary=os.path.join(ROOT, "oracle", "_ref", "blockchain_ref"), n_ref=a.ref) if a.ref else {}
     if a.ref:
         if a.difficulty != 9:
             ap.error("the reference binary mines at its DEFAULT_DIFFICULTY macro, 9")
-        extra = ("--pause-ms", "5")  # as the mixed test: GPU ranks leave the reference ranks room to win
+        # as the mixed test: GPU set-up before MPI_Init (reference ranks join no
+        # start barrier), and blocks 1-3 left to the reference ranks
+        extra = ("--serial-init", "1", "--idle-below", "3")
     walls, forks = [], 0
     for i in range(a.runs):
-        with tempfile.TemporaryDirectory() as wd:
+        with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as wd:
             t0 = time.perf_counter()
             run = run_network(a.ranks, wd, difficulty=a.difficulty, blocks=10, timeout=a.timeout, extra_args=extra,
                               **ref)
@@ -61,12 +67,15 @@ def main() -> int:
                 ok = False
         ok = ok and complete > 0
         n_fork = sum(run.stdout.count(m) for m in FORK_MSGS)
+        if a.forced_fork:
+            ok = ok and n_fork >= 1
         cross = ""
         if a.ref:  # blocks adopted across implementations (reference ranks are 0..ref-1)
             acc = [(int(r), int(s_)) for r, s_ in
                    re.findall(r"\[(\d+)\] Agregado a la lista bloque con index \d+ enviado por (\d+)", run.stdout)]
-            cross = (f", ref<-gpu {sum(r < a.ref <= s_ for r, s_ in acc)}"
-                     f", gpu<-ref {sum(s_ < a.ref <= r for r, s_ in acc)}")
+            n_rg, n_gr = sum(r < a.ref <= s_ for r, s_ in acc), sum(s_ < a.ref <= r for r, s_ in acc)
+            cross = f", ref<-gpu {n_rg}, gpu<-ref {n_gr}"
+            ok = ok and n_rg > 0 and n_gr > 0  # blocks crossed the implementations both ways
         forks += n_fork
         walls.append(wall)
         print(f"run {i + 1}/{a.runs}: rc {run.returncode} wall {wall:.2f} s, dumps {len(run.chains)}, "

@@ -27,7 +27,7 @@ runs = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 for (d, n), ref_s in PUBLISHED.items():
     walls, chains_ok = [], True
     for _ in range(runs):
-        with tempfile.TemporaryDirectory() as td:
+        with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
             t = time.perf_counter()
             run = run_network(n, td, difficulty=d, blocks=10, timeout=120)
             walls.append(time.perf_counter() - t)

@@ -23,13 +23,13 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 ref = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref")
 walls = {"reference": [], "gpu_serial_init": [], "gpu_overlapped_init": []}
 for r in range(reps):
-    with tempfile.TemporaryDirectory() as td:
+    with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
         t = time.perf_counter()
         p = subprocess.run(["timeout", "-k", "5", "120", MPIEXEC, "-np", "4", ref], cwd=td, env=mpi_env(),
                            capture_output=True, text=True)
         walls["reference"].append(time.perf_counter() - t)
     for name, extra in (("gpu_serial_init", ("--serial-init", 1)), ("gpu_overlapped_init", ())):
-        with tempfile.TemporaryDirectory() as td:
+        with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as td:
             t = time.perf_counter()
             run = run_network(4, td, difficulty=9, blocks=10, timeout=120, extra_args=extra)
             walls[name].append(time.perf_counter() - t)
