@@ -15,7 +15,8 @@ hashes).  Runtime: ~20 min on 8 cores.
 
 S1 (the realistic chained template of SURVEY.md §8c: index=7, owner=3,
 difficulty=9, created_at=1760572800, prev = a 64-char hex hash + NUL + zeros)
-goes to fingerprints_2p32_S1.json.  A non-zero start (e.g. 7 * 2^32: the window
+goes to fingerprints_2p32_S1.json; S2 (truncated header fields, prev = 64 x 'Z' +
+NUL + 191 x 'Z') to fingerprints_2p32_S2.json.  A non-zero start (e.g. 7 * 2^32: the window
 rank 7 sweeps in bench.py's 8-GPU run) goes to
 fingerprints_2p32_<template>_at<start>.json; counters in it are relative to start.
 """
@@ -38,7 +39,9 @@ L.oracle_sweep_lz.argtypes = [ctypes.POINTER(OBlock), ctypes.c_uint64, ctypes.c_
 L.oracle_sweep_lz.restype = ctypes.c_size_t
 TEMPLATES = {"S0": make_oblock(1, 0, 9, 1700000000, b""),
              "S1": make_oblock(7, 3, 9, 1760572800,
-                               b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")}
+                               b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8"),
+             # S2: every header field truncated to its low byte, non-zero prev tail
+             "S2": make_oblock(300, 7, 9, 0x1000000FF, b"Z" * 64 + b"\0" + b"Z" * 191)}
 S0 = TEMPLATES[which]
 cap = 9_000_000
 ctr = np.zeros(cap, np.uint32)
