@@ -323,15 +323,6 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // A 256-thread workgroup puts one wave on each SIMD of its CU.
   const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
-  L.consts_dev = nullptr;  // <= 64 workgroups: constants from the kernarg copy
-  if (grid > 64) {         // more: from a device copy (uploaded once per template)
-    if (ctx->consts_dirty) {
-      HIP_OK(hipMemcpyAsync(ctx->d_consts, &ctx->h_blob->consts, sizeof(PowConsts), hipMemcpyHostToDevice,
-                            ctx->stream));
-      ctx->consts_dirty = false;
-    }
-    L.consts_dev = ctx->d_consts;
-  }
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
   // One dispatch: constants by value (kernarg), result published by the
   // kernel's last wave into mapped host memory (no copy kernels).

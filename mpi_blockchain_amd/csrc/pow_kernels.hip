@@ -430,27 +430,27 @@ template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32
 // is static: with thousands of waves a shared atomic queue head (~88 dequeues
 // per us) would itself bound the rate.  K1 instead keeps the lowest
 // prefixes' wave busy for all 62 values of the last digit (~0.6 ms on an idle
-// SIMD).  Costs ~8% more VALU per trial than K1 (no j-uniform terms).
+// SIMD).  Costs ~5% more VALU per trial than K1 (no j-uniform terms).
 //
 // Launch overhead matters at this size (~17 us of kernel at d = 9), so the
 // constants travel as a by-value kernel argument (kernarg segment, read by
-// scalar loads like any constant) instead of a separate H2D copy for small
-// grids (L.consts_dev == null), the device
-// result words `res` reset themselves (the last wave to exit re-initialises
-// them), and that last wave also copies them to `hout`, mapped host memory:
-// a launch is one dispatch and no copy kernels.
+// scalar loads like any constant; chunks 1-4's K+W by one vector load per
+// thread into LDS) instead of a separate H2D copy, the device result words
+// `res` reset themselves (the last wave to exit re-initialises them), and that
+// last wave also copies them to `hout`, mapped host memory: a launch is one
+// dispatch and no copy kernels.
 template <bool FULL, bool ANY>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search_lat(
     const PowConsts C0, PowLaunchLat L, PowResult* __restrict__ res, PowResult* __restrict__ hout) {
   (void)C0;
   // C0 is the first kernel argument, at offset 0 of the kernarg segment: read
   // it through that (constant address space) pointer.  Taking C0's address
-  // would make the compiler copy 2.3 KB into private memory per lane.
-  // Small grids read the kernarg copy (no H2D copy before the launch); large
-  // ones a device copy: kernarg memory is slower to fetch when hundreds of CUs
-  // miss on it at once (d = 13, 256 workgroups: +7 us).
-  const cptr Cb = L.consts_dev ? as_const(reinterpret_cast<const uint32_t*>(L.consts_dev))
-                               : (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+  // would make the compiler copy 2.3 KB into private memory per lane.  Every
+  // grid reads the kernarg copy: since chunks 1-4's K+W moved to one vector
+  // load per thread (LDS copy), 256-1024 workgroups fetch it faster than an
+  // H2D copy (a blit kernel and a second dispatch) takes: time-to-block
+  // d = 13 0.0447 -> 0.0408 ms, d = 17 0.0578 -> 0.0544 ms (profiles/r02/ab/ab15).
+  const cptr Cb = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;

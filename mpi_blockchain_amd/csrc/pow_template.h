@@ -87,7 +87,6 @@ struct PowLaunchLat {
   uint32_t pad;
   uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
   PowWatch watch;
-  const PowConsts* consts_dev;  // null: read the by-value copy in the kernarg segment
 };
 
 struct PowLaunch {
