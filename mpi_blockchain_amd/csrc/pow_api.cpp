@@ -162,6 +162,8 @@ struct pow_ctx {
   int device = 0;
   int cu_count = 0;
   int clock_khz = 0;
+  int realtime_khz = 100000;  // s_memrealtime rate (hipDeviceAttributeWallClockRate)
+  uint32_t lat_seq = 0;       // K1' launches so far (PowLaunchLat::seq)
   char name[256] = {0};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -323,16 +325,27 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // A 256-thread workgroup puts one wave on each SIMD of its CU.
   const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
-  HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
+  if (++ctx->lat_seq == 0) ctx->lat_seq = 1;  // never 0: warm-up launches publish 0
+  L.seq = ctx->lat_seq;
   // One dispatch: constants by value (kernarg), result published by the
-  // kernel's last wave into mapped host memory (no copy kernels).
+  // kernel's last wave into mapped host memory (no copy kernels), `done` last.
   HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->h_blob->consts, L,
                                ctx->d_lat, ctx->d_lat_host));
-  HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
-  HIP_OK(hipStreamSynchronize(ctx->stream));
+  // Return as soon as the result is published: the kernel's completion
+  // signal reaches the host ~5 us after its last wave exits (rocprofv3 trace
+  // of tools/ttb_c).  A launch that ends without publishing
+  // (a fault) is caught by the stream query every 1024 polls.
+  for (uint32_t n = 1; __atomic_load_n(&ctx->h_lat->done, __ATOMIC_ACQUIRE) != L.seq; ++n) {
+    if ((n & 1023u) == 0) {
+      const hipError_t q = hipStreamQuery(ctx->stream);
+      if (q == hipErrorNotReady) continue;
+      if (__atomic_load_n(&ctx->h_lat->done, __ATOMIC_ACQUIRE) == L.seq) break;
+      HIP_OK(q);
+      return fail(POW_EHIP, "latency kernel ended without publishing its result");
+    }
+  }
   memcpy(ctx->h_res, (const void*)ctx->h_lat, sizeof(PowResult));
-  float ms = 0;
-  HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  const double ms = (double)ctx->h_res->ticks / ctx->realtime_khz;
   ctx->stats.kernel_ms += ms;
   ctx->stats.launches += 1;
   ctx->stats.hashes += ctx->h_res->hashes;
@@ -424,6 +437,11 @@ int pow_init(int device, pow_ctx** out) {
   pow_ctx* ctx = new pow_ctx;
   ctx->device = device;
   ctx->cu_count = prop.multiProcessorCount;
+  {
+    int rt = 0;
+    if (hipDeviceGetAttribute(&rt, hipDeviceAttributeWallClockRate, device) == hipSuccess && rt > 0)
+      ctx->realtime_khz = rt;
+  }
   ctx->clock_khz = prop.clockRate;
   snprintf(ctx->name, sizeof ctx->name, "%s", prop.name);
   // 8 x 256-thread WGs = 32 waves/CU fill the chip; one slot stays free so

@@ -458,6 +458,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   bool wrote_hit = false;  // this wave wrote a hit record (wave-uniform after each step)
   __shared__ uint32_t wg_iters;  // wave-iterations of this workgroup
   if (threadIdx.x == 0) wg_iters = 0;
+  // The launch's duration is measured on the GPU (constant-rate realtime
+  // counter): the host returns when `done` is published, not at the kernel's
+  // completion signal, so it records no HIP events around the launch.
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(&res->t_start, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // chunks 1-4's K+W words (PowConsts::kw), one per thread, as in K1
   __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
   lkw[threadIdx.x] = Cb[threadIdx.x];
@@ -555,7 +560,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   // of microseconds.  Only waves that wrote hit records release them (an
   // agent-scope release writes back L2); min_rel and nhit are atomics.  The
   // last workgroup acquires.
-  if (wrote_hit) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (wrote_hit || blockIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   if (lane == 0) atomicAdd(&wg_iters, iters);
   __syncthreads();
   if (threadIdx.x < 64u) {
@@ -577,6 +582,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         hout->hashes = ((old >> 32) + wg_iters) * 64ull;
         hout->nhit = res->nhit;
         hout->cancelled = res->cancelled;
+        hout->ticks = __builtin_amdgcn_s_memrealtime() -
+                      __hip_atomic_load(&res->t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         res->min_rel = ~0ull;
         res->hashes = 0;
         res->nhit = 0;
@@ -584,6 +591,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
         res->peer_abs = ~0ull;
       }
       __threadfence_system();
+      if (lane == 0) __hip_atomic_store(&hout->done, L.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

@@ -84,7 +84,7 @@ struct PowLaunchLat {
   uint32_t base_digit[9];  // base-62 digits of ctr_start (nonce[0..8])
   uint32_t thr;            // as PowLaunch
   uint32_t diff;
-  uint32_t pad;
+  uint32_t seq;            // launch sequence number, published last (PowResult::done)
   uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
   PowWatch watch;
 };
@@ -124,6 +124,10 @@ struct PowResult {
   unsigned int cancelled;      // set once a sentinel wave saw host_epoch != launch_epoch
   unsigned long long peer_abs; // lowest counter a peer published on the board (sentinel wave), ~0 = none
   PowWatch watch;              // K1 mine modes (K1' takes it in its launch parameters)
+  unsigned long long t_start;  // K1': s_memrealtime at workgroup 0's start ...
+  unsigned long long ticks;    // ... and the last workgroup's exit minus it (published)
+  unsigned int done;           // K1': the launch's seq, stored last (system scope): the host
+  unsigned int pad1;           //      polls it instead of waiting for the completion signal
   PowHit hit[POW_HITS];
 };
 
