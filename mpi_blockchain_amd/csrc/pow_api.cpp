@@ -37,13 +37,16 @@ static_assert(offsetof(PowConsts, w3) == 4 * PC_W3, "PC_W3");
 static_assert(offsetof(PowConsts, k) == 4 * PC_K, "PC_K");
 static_assert(offsetof(PowConsts, st0) == 4 * PC_ST0, "PC_ST0");
 static_assert(offsetof(PowConsts, w0raw) == 4 * PC_WRAW, "PC_WRAW");
+static_assert(offsetof(PowConstsLat, st0) == 4 * LC_ST0 && offsetof(PowConstsLat, kw0) == 4 * LC_KW0 &&
+                  offsetof(PowConstsLat, k) == 4 * LC_K && offsetof(PowConstsLat, w0raw) == 4 * LC_WRAW,
+              "LC_*");
 
 hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream, const PowConsts* C,
                              const PowLaunch& L, uint32_t* out, PowResult* res);
 hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
 hipError_t pow_sort_u32(void* temp, size_t* temp_bytes, uint32_t* keys, uint32_t* alt, uint32_t n,
                         uint32_t** sorted, hipStream_t stream);
-hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConsts& C,
+hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConstsLat& C,
                                  const PowLaunchLat& L, PowResult* res, PowResult* hout);
 
 namespace {
@@ -164,6 +167,7 @@ struct pow_ctx {
   int clock_khz = 0;
   int realtime_khz = 100000;  // s_memrealtime rate (hipDeviceAttributeWallClockRate)
   uint32_t lat_seq = 0;       // K1' launches so far (PowLaunchLat::seq)
+  PowConstsLat lat_consts{};  // K1''s kernel argument (the subset of h_blob->consts it reads)
   char name[256] = {0};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -329,7 +333,7 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   L.seq = ctx->lat_seq;
   // One dispatch: constants by value (kernarg), result published by the
   // kernel's last wave into mapped host memory (no copy kernels), `done` last.
-  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->h_blob->consts, L,
+  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->lat_consts, L,
                                ctx->d_lat, ctx->d_lat_host));
   // Return as soon as the result is published: the kernel's completion
   // signal reaches the host ~5 us after its last wave exits (rocprofv3 trace
@@ -356,6 +360,13 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
 // uploads them together with its result words (one H2D copy).
 int upload_consts(pow_ctx* ctx, const pow_block* tmpl) {
   pow_build_consts(tmpl, &ctx->h_blob->consts);
+  const PowConsts& C = ctx->h_blob->consts;
+  PowConstsLat& Q = ctx->lat_consts;
+  memcpy(Q.kw, C.kw, sizeof Q.kw);
+  memcpy(Q.st0, C.st0, sizeof Q.st0);
+  memcpy(Q.kw0, C.kw0, sizeof Q.kw0);
+  memcpy(Q.k, C.k, sizeof Q.k);
+  memcpy(Q.w0raw, C.w0raw, sizeof Q.w0raw);
   ctx->consts_dirty = true;
   return POW_OK;
 }
@@ -530,7 +541,7 @@ int pow_warmup(pow_ctx* ctx) {
       HIP_OK(pow_launch_search(mode, full != 0, 1, ctx->stream, ctx->d_consts, L, nullptr, ctx->d_res));
   for (int any = 0; any < 2; ++any)
     for (int full = 0; full < 2; ++full)
-      HIP_OK(pow_launch_search_lat(full != 0, any != 0, 1, ctx->stream, ctx->h_blob->consts, LL, ctx->d_lat,
+      HIP_OK(pow_launch_search_lat(full != 0, any != 0, 1, ctx->stream, ctx->lat_consts, LL, ctx->d_lat,
                                    ctx->d_lat_host));
   HIP_OK(pow_launch_hash(0, ctx->stream, nullptr, nullptr));
   HIP_OK(hipStreamSynchronize(ctx->stream));

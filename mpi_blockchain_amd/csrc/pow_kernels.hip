@@ -440,12 +440,12 @@ template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32
 // last wave also copies them to `hout`, mapped host memory: a launch is one
 // dispatch and no copy kernels.
 template <bool FULL, bool ANY>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_search_lat(
-    const PowConsts C0, PowLaunchLat L, PowResult* __restrict__ res, PowResult* __restrict__ hout) {
+__global__ __launch_bounds__(256) void pow_search_lat(
+    const PowConstsLat C0, PowLaunchLat L, PowResult* __restrict__ res, PowResult* __restrict__ hout) {
   (void)C0;
   // C0 is the first kernel argument, at offset 0 of the kernarg segment: read
   // it through that (constant address space) pointer.  Taking C0's address
-  // would make the compiler copy 2.3 KB into private memory per lane.  Every
+  // would make the compiler copy 1.4 KB into private memory per lane.  Every
   // grid reads the kernarg copy: since chunks 1-4's K+W moved to one vector
   // load per thread (LDS copy), 256-1024 workgroups fetch it faster than an
   // H2D copy (a blit kernel and a second dispatch) takes: time-to-block
@@ -492,24 +492,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
     cptr P = pin(Cb, rel);
     uint32_t w[64];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = P[PC_WRAW + i];
+    for (int i = 0; i < 16; ++i) w[i] = P[LC_WRAW + i];
     w[1] = (digit_char(dg[0]) << 24) | (digit_char(dg[1]) << 16) | (digit_char(dg[2]) << 8) | digit_char(dg[3]);
     w[2] = (digit_char(dg[4]) << 24) | (digit_char(dg[5]) << 16) | (digit_char(dg[6]) << 8) | digit_char(dg[7]);
     w[3] |= digit_char(dg[8]) << 24;  // [nonce[8], NUL, prev0, prev1]
-    St s{P[PC_ST0 + 0], P[PC_ST0 + 1], P[PC_ST0 + 2], P[PC_ST0 + 3],
-         P[PC_ST0 + 4], P[PC_ST0 + 5], P[PC_ST0 + 6], P[PC_ST0 + 7]};  // after round 0
-    round_k_w_o(s, P[PC_K + 1], w[1]);
-    round_k_w_o(s, P[PC_K + 2], w[2]);
-    round_k_w_o(s, P[PC_K + 3], w[3]);
+    St s{P[LC_ST0 + 0], P[LC_ST0 + 1], P[LC_ST0 + 2], P[LC_ST0 + 3],
+         P[LC_ST0 + 4], P[LC_ST0 + 5], P[LC_ST0 + 6], P[LC_ST0 + 7]};  // after round 0
+    round_k_w_o(s, P[LC_K + 1], w[1]);
+    round_k_w_o(s, P[LC_K + 2], w[2]);
+    round_k_w_o(s, P[LC_K + 3], w[3]);
 #pragma unroll
-    for (int i = 4; i < 16; ++i) round_kw_o(s, P[PC_KW0 + i]);
-    cptr Kp = pin(Cb + PC_K, s.e);
+    for (int i = 4; i < 16; ++i) round_kw_o(s, P[LC_KW0 + i]);
+    cptr Kp = pin(Cb + LC_K, s.e);
 #pragma unroll
     for (int i = 16; i < 40; ++i) {
       w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
       round_k_w_o(s, Kp[i], w[i]);
     }
-    cptr K2 = pin(Cb + PC_K, s.e);
+    cptr K2 = pin(Cb + LC_K, s.e);
 #pragma unroll
     for (int i = 40; i < 64; ++i) {
       w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
@@ -596,10 +596,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void pow_
   }
 }
 
-template __global__ void pow_search_lat<false, false>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
-template __global__ void pow_search_lat<true, false>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
-template __global__ void pow_search_lat<false, true>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
-template __global__ void pow_search_lat<true, true>(const PowConsts, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
 
 // K2: block_to_hash for n blocks; `msgs` holds each block's 270-byte message
 // already padded on the host to 320 bytes (80 big-endian words).
@@ -637,7 +637,7 @@ extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hi
 }
 
 extern "C++" hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream,
-                                              const PowConsts& C, const PowLaunchLat& L, PowResult* res,
+                                              const PowConstsLat& C, const PowLaunchLat& L, PowResult* res,
                                               PowResult* hout) {
   dim3 g(grid), b(256);
   if (!full && !any) hipLaunchKernelGGL((pow_search_lat<false, false>), g, b, 0, stream, C, L, res, hout);

@@ -45,6 +45,21 @@ struct PowConsts {
   uint32_t w0raw[16];    // chunk-0 words as hashed (W1..W3 = 0 placeholders; latency kernel)
 };
 
+// The part of PowConsts the latency kernel K1' reads, passed by value as its
+// kernel argument (1.4 KB of kernarg instead of 2.7 KB: the j-uniform tables
+// and schedule partial sums are K1's alone).
+struct PowConstsLat {
+  uint32_t kw[4][64];   // = PowConsts::kw
+  uint32_t st0[8];      // = PowConsts::st0
+  uint32_t kw0[16];     // = PowConsts::kw0
+  uint32_t k[64];       // = PowConsts::k
+  uint32_t w0raw[16];   // = PowConsts::w0raw
+};
+#define LC_ST0 256
+#define LC_KW0 (LC_ST0 + 8)
+#define LC_K (LC_KW0 + 16)
+#define LC_WRAW (LC_K + 64)
+
 // Word offsets into PowConsts for the kernel's constant-address-space loads.
 #define PC_ST0 256
 #define PC_KW0 (PC_ST0 + 8)
