@@ -75,7 +75,10 @@ enum {
 
 /* Per-call statistics of the last pow_mine / pow_sweep / pow_hash_blocks. */
 typedef struct pow_stats {
-  double kernel_ms;      /* sum of HIP-event-timed kernel durations on the ctx stream */
+  double kernel_ms;      /* sum of kernel durations on the ctx stream: HIP events around the
+                            sweep/mine kernels; the latency kernel (first sub-round of
+                            pow_mine[_any] at d <= 21) times itself with the GPU's realtime
+                            counter, from workgroup 0's start to the last workgroup's exit */
   uint32_t launches;     /* kernels launched by the call */
   uint64_t hashes;       /* trials issued to the GPU (incl. edge lanes masked out) */
 } pow_stats;
