@@ -132,6 +132,7 @@ class Node {
   pow_ctx* mine_ctx_ = nullptr;              // used only by the mining thread
   pow_ctx* recv_ctx_ = nullptr;              // used only by the receive thread
   std::deque<std::pair<pow_block, MPI_Status>> deferred_;
+  std::atomic<int> rivals1_{0};  // --hold-first: peers' blocks 1 this rank has processed
 
   // The chain moved: a running pow_mine_any on the old template stops at its
   // next GPU poll (pow_cancel), not at its next sub-round (up to ~0.13 s).
@@ -395,6 +396,14 @@ class Node {
           std::lock_guard<std::mutex> g(mu_);
           send_block_to_everyone(blocks_.at(hash_of(solved)));
         }
+        // ... and mine block 2 only once every peer's block 1 has been through
+        // validate_block_for_chain here: otherwise, with blocks taking ~20 us
+        // at d = 5, a fast rank can finish the chain (MPI_Abort) before a slow
+        // receive thread has handled (and logged) its rival block 1.  Bounded
+        // wait: a peer whose block 1 never comes (it adopted ours first) does
+        // not hold the network up past 2 s.
+        for (int w = 0; w < 40000 && rivals1_.load(std::memory_order_acquire) < size_ - 1; ++w)
+          std::this_thread::sleep_for(std::chrono::microseconds(50));
       } else if (rc == 1) {  // node.cpp:311-327
         std::lock_guard<std::mutex> g(mu_);
         if (last_->index < solved.index) {
@@ -477,6 +486,7 @@ int Node::run() {
     std::lock_guard<std::mutex> g(mu_);
     if (st.MPI_TAG == kTagNewBlock) {
       validate_block_for_chain(buf, st);
+      if (buf.index == 1) rivals1_.fetch_add(1, std::memory_order_release);
     } else if (st.MPI_TAG == kTagChainHash) {
       printf("[%u] TAG_CHAIN_HASH \n", rank_);
       send_blockchain(buf, st.MPI_SOURCE);
