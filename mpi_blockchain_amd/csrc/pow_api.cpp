@@ -5,6 +5,7 @@
 // block_to_hash (block.cpp:74-77); see include/pow_gpu.h for the mapping of
 // each entry point to the reference function it replaces.
 #include <hip/hip_runtime.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -19,6 +20,10 @@
 
 #include "../../include/pow_gpu.h"
 #include "pow_template.h"
+
+#ifndef POW_WAIT_POLL_US
+#define POW_WAIT_POLL_US 50  // long launches: host poll period (us) of the completion event
+#endif
 
 static_assert(sizeof(pow_block) == 552, "pow_block must match block.h:17-25 (LP64)");
 static_assert(offsetof(pow_block, created_at) == 16, "layout");
@@ -296,11 +301,18 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   // Synchronize spins, blocking-sync event or not).  At most 50 us late on a
   // >= 8 ms launch.  Short launches keep the spin wait: their latency is the
   // whole time-to-block at low difficulty.
+  // The calling thread's timer slack (50 us by default on Linux) is lowered
+  // to 1 us for the wait: a 50 us sleep otherwise lasts ~100 us, and the end
+  // of a pow_mine_any launch that found a block at d = 25 was seen 50-75 us
+  // late (rocprofv3 HIP trace of tools/ttb_c 25).
   if (count >= (1ull << 26)) {
     HIP_OK(hipEventRecord(ctx->ev_block, ctx->stream));
+    const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+    if (slack > 1000) prctl(PR_SET_TIMERSLACK, 1000ul, 0, 0, 0);
     hipError_t q;
     while ((q = hipEventQuery(ctx->ev_block)) == hipErrorNotReady)
-      std::this_thread::sleep_for(std::chrono::microseconds(50));
+      std::this_thread::sleep_for(std::chrono::microseconds(POW_WAIT_POLL_US));
+    if (slack > 1000) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
     HIP_OK(q);
   }
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -338,9 +350,9 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // Return as soon as the result is published: the kernel's completion
   // signal reaches the host ~5 us after its last wave exits (rocprofv3 trace
   // of tools/ttb_c).  A launch that ends without publishing
-  // (a fault) is caught by the stream query every 1024 polls.
+  // (a fault) is caught by a stream query every 65536 polls.
   for (uint32_t n = 1; __atomic_load_n(&ctx->h_lat->done, __ATOMIC_ACQUIRE) != L.seq; ++n) {
-    if ((n & 1023u) == 0) {
+    if ((n & 0xFFFFu) == 0) {  // every ~60 us
       const hipError_t q = hipStreamQuery(ctx->stream);
       if (q == hipErrorNotReady) continue;
       if (__atomic_load_n(&ctx->h_lat->done, __ATOMIC_ACQUIRE) == L.seq) break;

@@ -5,7 +5,7 @@
  * rate (sum of trials / sum of HIP-event kernel time over all calls).
  *
  *   gcc -O2 -I include tools/ab_ttb.c -ldl -o tools/ab_ttb
- *   tools/ab_ttb <d> <templates> a/libpow_gpu.so b/libpow_gpu.so ...       */
+ *   [AB_TTB_LOWEST=1] tools/ab_ttb <d> <templates> a/libpow_gpu.so b/libpow_gpu.so ...  */
 #include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -52,7 +52,10 @@ int main(int argc, char** argv) {
     }
     init_fn init = (init_fn)dlsym(h, "pow_init");
     warm_fn warm = (warm_fn)dlsym(h, "pow_warmup");
-    mine[v] = (any_fn)dlsym(h, "pow_mine_any");
+    /* AB_TTB_LOWEST=1: pow_mine (lowest solving counter: the same work on
+     * every library, so the wall times pair up exactly) */
+    const char* lo = getenv("AB_TTB_LOWEST");
+    mine[v] = (any_fn)dlsym(h, lo && lo[0] == '1' ? "pow_mine" : "pow_mine_any");
     stats[v] = (stats_fn)dlsym(h, "pow_get_stats");
     if (!init || !warm || !mine[v] || !stats[v] || init(0, &ctx[v]) || warm(ctx[v])) {
       fprintf(stderr, "init failed for %s\n", argv[3 + v]);
