@@ -209,6 +209,7 @@ struct pow_ctx {
   unsigned grid_full = 0;  // workgroups that fill the chip (8 per CU)
   bool force_full = false; // POW_FORCE_FULL=1: use the d > 32 kernel for every d (tests)
   uint64_t lat_max = 1ull << 24;  // POW_LAT_MAX: first-sub-round cap for K1' (0 = K1 only)
+  unsigned lat_wps = 0;           // POW_LAT_WPS (tuning runs): K1' waves per SIMD at every d (0 = plan)
   pow_stats stats{};
 };
 
@@ -473,6 +474,7 @@ int pow_init(int device, pow_ctx** out) {
   ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u - 1u;
   if (const char* ff = getenv("POW_FORCE_FULL")) ctx->force_full = ff[0] == '1';
   if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
+  if (const char* lw = getenv("POW_LAT_WPS")) ctx->lat_wps = (unsigned)std::min(8ul, strtoul(lw, nullptr, 0));
   if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
     const int per = atoi(g);
     if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
@@ -757,7 +759,7 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   //    expected trials and grow 4x.
   const unsigned dcap = diff_bits > 40 ? 40 : diff_bits;
   const bool use_lat = ctx->lat_max > 0 && diff_bits <= 21;
-  const unsigned lat_wps = diff_bits <= 17 ? 1 : diff_bits <= 19 ? 2 : 4;
+  const unsigned lat_wps = ctx->lat_wps ? ctx->lat_wps : diff_bits <= 17 ? 1 : diff_bits <= 19 ? 2 : 4;
   uint64_t step = use_lat ? std::max<uint64_t>(1ull << 12, 1ull << (dcap + 4))
                           : (any ? 1ull << 30 : std::max<uint64_t>(1ull << 12, 1ull << std::min(dcap + 2, 30u)));
   // Bound stop board: a peer's solution makes the rest of the range moot —
