@@ -170,6 +170,27 @@ def test_mine_any_returns_a_solution(mminer, golden, templates):
             assert 256 - int(hx, 16).bit_length() >= int(d)
 
 
+def test_latency_kernel_timing_and_stats(miner, templates):
+    """The latency kernel times itself on the GPU (realtime counter from
+    workgroup 0's start to the last workgroup's exit) and the host returns on
+    its published `done` word: kernel_ms is positive and below the call's wall
+    time, one launch per call at low d, and the trial count covers the winner."""
+    import time
+
+    b = block_from_template(templates["S0"])
+    for d, want in ((9, 238), (13, None)):
+        t = time.perf_counter()
+        r = miner.mine(b, 0, 1 << 24, d)
+        wall_ms = 1e3 * (time.perf_counter() - t)
+        st = miner.stats()
+        assert r is not None and (want is None or r.counter == want)
+        assert 0 < st["kernel_ms"] < wall_ms, (st, wall_ms)
+        assert st["launches"] >= 1 and st["hashes"] > r.counter, st
+    # back-to-back calls: every launch publishes its own sequence number
+    got = [miner.mine(b, 0, 1 << 16, 9).counter for _ in range(50)]
+    assert got == [238] * 50
+
+
 def test_mine_no_solution_and_bounds(miner, templates):
     b = block_from_template(templates["S0"])
     assert miner.mine(b, 0, 200, 9) is None  # first S0 solution is 238
