@@ -194,16 +194,24 @@ def pmc_traffic_live(timeout: float = 120) -> dict:
                    "--kernel-include-regex", "pow_search", "-d", td, "-o", "run", "--", SWEEP_TOOL, "2", lib]
             p = subprocess.run(cmd, cwd=td, capture_output=True, text=True, timeout=timeout + 30,
                                env=dict(os.environ, TMPDIR="/tmp"))
-            per = {}
+            per, grid = {}, {}
             for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
                     if "pow_search<0, false>" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                         per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-            # pow_warmup's empty launch of the same kernel is a dispatch too: drop it
-            vals = sorted(v for v in per.values() if per and v >= 0.01 * max(per.values()))
+                        grid[r["Dispatch_Id"]] = int(r.get("Grid_Size") or 0)
+            # pow_warmup's empty launch of the same kernel (one workgroup) is a
+            # dispatch too: keep the full-chip sweeps only.  Without a grid
+            # column, drop what is far below the median (not the max: one
+            # dispatch in a few reads tens of MB more, r02's pmc_summary.json).
+            if per and all(grid.values()):
+                vals = sorted(v for k, v in per.items() if grid[k] > 64 * 256)
+            else:
+                med = sorted(per.values())[len(per) // 2] if per else 0.0
+                vals = sorted(v for v in per.values() if v >= 0.01 * med)
             if p.returncode != 0 or len(vals) < 3:
-                return {"error": f"{counter} pass rc {p.returncode}, {len(vals)} sweep dispatches: "
-                                 + (p.stderr or "")[-200:]}
+                return {"error": f"{counter} pass rc {p.returncode}, {len(vals)} sweep dispatches "
+                                 f"(all: {sorted(per.values())}): " + (p.stderr or "")[-200:]}
             out[counter] = {"kib_per_dispatch": vals, "median_bytes": int(vals[len(vals) // 2] * 1024)}
     out["total_bytes"] = out["FETCH_SIZE"]["median_bytes"] + out["WRITE_SIZE"]["median_bytes"]
     return out
