@@ -112,26 +112,36 @@ def cpu_baseline(seconds: float = 1.5) -> dict | None:
             out[key] = json.loads(r.stdout.strip().splitlines()[-1])
         except Exception as e:  # pragma: no cover
             out[key] = {"error": str(e)[-300:]}
-    if "O2" in out and "trials_per_s" in out["O2"]:
-        o2 = out["O2"]
-        launch = (f"mpiexec -np {ranks} (one MPI rank per CPU)" if how == "mpi"
-                  else f"{ranks} forked processes (one per CPU)")
-        res = {"value": round(o2["trials_per_s"], 1), "unit": "trials/s", "cores": ranks, "kind": "reference",
+    good = {k: v for k, v in out.items() if "trials_per_s" in v and k.startswith("O2")}
+    if good:
+        # Headline: the best rate the reference loop reaches on this job's CPUs
+        # (with a cgroup quota below the affinity mask, 256 ranks throttled onto
+        # 16 CPUs' worth of time lose to the at-quota run); `cores` = the CPUs
+        # the job can actually use, logical and physical counts beside it.
+        key = max(good, key=lambda k: good[k]["trials_per_s"])
+        best = good[key]
+        nranks = best.get("ranks", best.get("procs", ranks))
+        launch = (f"mpiexec -np {nranks} (one MPI rank per CPU{' of the cgroup quota' if key == 'O2_at_quota' else ''})"
+                  if how == "mpi" else f"{nranks} forked processes")
+        try:
+            physical = int(host["sockets"]) * int(host["cores_per_socket"])
+        except Exception:
+            physical = None
+        res = {"value": round(best["trials_per_s"], 1), "unit": "trials/s", "cores": int(round(usable)),
+               "kind": "reference",
                "sample": (f"reference proof_of_work loop body (node.cpp:292-308; /root/reference block.cpp + "
                           f"picosha2.h built -O2 by oracle/Makefile), {launch} x {seconds} s, rand() nonces, "
-                          f"difficulty 9")}
-        res["per_core"] = round(o2["trials_per_s"] / ranks, 1)
-        # With a CPU quota below the affinity mask the ranks share `usable` CPUs' worth of time.
-        res["per_usable_cpu"] = round(o2["trials_per_s"] / usable, 1)
+                          f"difficulty 9; the best of the runs in `runs`"),
+               "per_core": round(best["trials_per_s"] / max(1.0, usable), 1),
+               "logical_cpus": host["affinity"], "physical_cores": physical,
+               "usable_cpus": usable, "headline_run": key,
+               "runs": {k: ({"ranks": v.get("ranks", v.get("procs")), "trials_per_s": round(v["trials_per_s"], 1)}
+                            if "trials_per_s" in v else v) for k, v in out.items()}}
         if "O0" in out and "trials_per_s" in out["O0"]:
             res["as_shipped_O0"] = round(out["O0"]["trials_per_s"], 1)
-            res["as_shipped_O0_per_usable_cpu"] = round(out["O0"]["trials_per_s"] / usable, 1)
         if "O2_at_quota" in out and "trials_per_s" in out["O2_at_quota"]:
             q = out["O2_at_quota"]
-            res["at_cpu_quota"] = {"ranks": q.get("ranks", q.get("procs")), "value": round(q["trials_per_s"], 1),
-                                   "per_rank": round(q["trials_per_s"] / max(1, q.get("ranks", q.get("procs", 1))), 1),
-                                   "note": "-O2, one rank per CPU of the cgroup quota: 256 ranks on 16 CPUs' worth "
-                                           "of time lose to throttling"}
+            res["at_cpu_quota"] = {"ranks": q.get("ranks", q.get("procs")), "value": round(q["trials_per_s"], 1)}
         res["host_cpus"] = dict(host, ranks=ranks, usable=usable)
         return res
     # restatement fallback ("port")
@@ -160,7 +170,7 @@ PMC_SUMMARY = os.path.join("profiles", "r02", "final", "pmc_summary.json")
 def pmc_traffic_committed():
     """HBM bytes per dispatch of this workload from the committed summary of
     tools/profile_round.sh's rocprofv3 passes (same command and build): the
-    fallback when the in-run passes (pmc_traffic_live) cannot run."""
+    fallback when the in-run passes (pmc_live) cannot run."""
     try:
         return int(json.load(open(os.path.join(ROOT, PMC_SUMMARY)))["hbm_bytes_per_dispatch"]["total"])
     except Exception:
@@ -170,50 +180,91 @@ def pmc_traffic_committed():
 SWEEP_TOOL = os.path.join(ROOT, "tools", "ab_sweep")  # built by __graft_entry__.build()
 
 
-def pmc_traffic_live(timeout: float = 120) -> dict:
-    """HBM traffic of the bench kernel measured now, on this box and build:
-    two rocprofv3 passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass on
-    gfx950), each over tools/ab_sweep sweeping S0's 2^32 window at d = 9 with
-    this libpow_gpu.so three times (warm-up + 2).  Per dispatch of
-    pow_search<0, false>, median of the 3; the counters are in KiB of 64-B
-    memory-side requests (MI355X_MICROARCH.md, HBM/rocprofv3 section; the kernel
-    has no wide streaming loads, so FETCH_SIZE needs no 2x correction)."""
+def _pmc_pass(prof: str, counters: list[str], timeout: float, trace: bool) -> tuple[dict, dict, str]:
+    """One rocprofv3 --pmc pass over tools/ab_sweep (S0's 2^32 window at d = 9,
+    warm-up + 2 sweeps, this build's libpow_gpu.so).  Per sweep dispatch of
+    pow_search<0, false>: {counter: value} and (with `trace`, --kernel-trace in
+    the same pass) the duration in ns."""
     import csv
     import glob
-    import shutil
     import tempfile
 
-    prof = shutil.which("rocprofv3")
     lib = os.path.join(ROOT, "mpi_blockchain_amd", "libpow_gpu.so")
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        cmd = ["timeout", "-s", "KILL", str(int(timeout)), prof, "--pmc", *counters,
+               *(["--kernel-trace"] if trace else []), "-f", "csv",
+               "--kernel-include-regex", "pow_search", "-d", td, "-o", "run", "--", SWEEP_TOOL, "2", lib]
+        p = subprocess.run(cmd, cwd=td, capture_output=True, text=True, timeout=timeout + 30,
+                           env=dict(os.environ, TMPDIR="/tmp"))
+        per, grid, dur = {}, {}, {}
+        for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "pow_search<0, false>" in r["Kernel_Name"] and r["Counter_Name"] in counters:
+                    d = per.setdefault(r["Dispatch_Id"], {})
+                    d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                    grid[r["Dispatch_Id"]] = int(r.get("Grid_Size") or 0)
+        for f in glob.glob(os.path.join(td, "**", "*kernel_trace.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "pow_search<0, false>" in r["Kernel_Name"]:
+                    dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    # pow_warmup's empty launch of the same kernel (one workgroup) is a dispatch
+    # too: keep the full-chip sweeps only (by grid size; without a grid column,
+    # drop what is far below the median, not the max: one dispatch in a few reads
+    # tens of MB more, r02's pmc_summary.json).
+    c0 = counters[0]
+    if per and all(grid.values()):
+        keep = [k for k in per if grid[k] > 64 * 256]
+    else:
+        med = sorted(v[c0] for v in per.values())[len(per) // 2] if per else 0.0
+        keep = [k for k, v in per.items() if v[c0] >= 0.01 * med]
+    keep.sort(key=lambda k: per[k][c0])
+    err = "" if p.returncode == 0 and len(keep) >= 3 else \
+        (f"{' '.join(counters)} pass rc {p.returncode}, {len(keep)} sweep dispatches: " + (p.stderr or "")[-200:])
+    return {k: per[k] for k in keep}, {k: dur[k] for k in keep if k in dur}, err
+
+
+def pmc_live(cu_count: int, timeout: float = 120) -> dict:
+    """Counters of the bench kernel measured now, on this box and build, in
+    three rocprofv3 passes (their counters do not fit one pass on gfx950):
+      * FETCH_SIZE, then WRITE_SIZE: HBM traffic per dispatch.  Both count KiB
+        of 64-B memory-side requests (MI355X_MICROARCH.md, HBM/rocprofv3
+        section); the kernel has no wide streaming loads, so FETCH_SIZE needs no
+        2x correction.  Median per dispatch of the 3 sweeps.
+      * SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE with the kernel
+        trace of the same dispatches: VALU wave-instructions per hash, the
+        clock the chip held (GRBM_GUI_ACTIVE is summed over the 8 XCDs) and the
+        SIMD cycles per VALU instruction.  The dispatch with the median
+        duration."""
+    import shutil
+
+    prof = shutil.which("rocprofv3")
     if not prof or not os.access(SWEEP_TOOL, os.X_OK):
         return {"error": "rocprofv3 or tools/ab_sweep missing"}
     out = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        with tempfile.TemporaryDirectory(dir="/tmp") as td:
-            cmd = ["timeout", "-s", "KILL", str(int(timeout)), prof, "--pmc", counter, "-f", "csv",
-                   "--kernel-include-regex", "pow_search", "-d", td, "-o", "run", "--", SWEEP_TOOL, "2", lib]
-            p = subprocess.run(cmd, cwd=td, capture_output=True, text=True, timeout=timeout + 30,
-                               env=dict(os.environ, TMPDIR="/tmp"))
-            per, grid = {}, {}
-            for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
-                for r in csv.DictReader(open(f)):
-                    if "pow_search<0, false>" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                        per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-                        grid[r["Dispatch_Id"]] = int(r.get("Grid_Size") or 0)
-            # pow_warmup's empty launch of the same kernel (one workgroup) is a
-            # dispatch too: keep the full-chip sweeps only.  Without a grid
-            # column, drop what is far below the median (not the max: one
-            # dispatch in a few reads tens of MB more, r02's pmc_summary.json).
-            if per and all(grid.values()):
-                vals = sorted(v for k, v in per.items() if grid[k] > 64 * 256)
-            else:
-                med = sorted(per.values())[len(per) // 2] if per else 0.0
-                vals = sorted(v for v in per.values() if v >= 0.01 * med)
-            if p.returncode != 0 or len(vals) < 3:
-                return {"error": f"{counter} pass rc {p.returncode}, {len(vals)} sweep dispatches "
-                                 f"(all: {sorted(per.values())}): " + (p.stderr or "")[-200:]}
-            out[counter] = {"kib_per_dispatch": vals, "median_bytes": int(vals[len(vals) // 2] * 1024)}
+        per, _, err = _pmc_pass(prof, [counter], timeout, trace=False)
+        if err:
+            return {"error": err}
+        vals = sorted(v[counter] for v in per.values())
+        out[counter] = {"kib_per_dispatch": vals, "median_bytes": int(vals[len(vals) // 2] * 1024)}
     out["total_bytes"] = out["FETCH_SIZE"]["median_bytes"] + out["WRITE_SIZE"]["median_bytes"]
+    vc = ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"]
+    per, dur, err = _pmc_pass(prof, vc, timeout, trace=True)
+    if err or not dur:
+        out["valu"] = {"error": err or "no kernel-trace rows"}
+        return out
+    ks = sorted(dur, key=dur.get)
+    k = ks[len(ks) // 2]
+    c, t_ns = per[k], dur[k]
+    clock = c["GRBM_GUI_ACTIVE"] / 8 / (t_ns * 1e-9)
+    out["valu"] = {"counters": c, "kernel_ns": t_ns, "dispatches": len(per),
+                   "valu_instr_per_hash": round(c["SQ_INSTS_VALU"] * 64 / WINDOW, 1),
+                   "clock_ghz": round(clock / 1e9, 4),
+                   # counter_defs.yaml's VALUBusy (gfx94x formula: every VALU
+                   # instruction priced at 4 cycles of one SIMD), > 100 % on
+                   # gfx950's SIMD-32, where a full-rate instruction takes 2
+                   "valu_busy_pct": round(100 * c["SQ_ACTIVE_INST_VALU"] / cu_count / (c["GRBM_GUI_ACTIVE"] / 8), 1),
+                   "cycles_per_valu_instr": round(4 * cu_count * clock * t_ns * 1e-9 / c["SQ_INSTS_VALU"], 3)}
     return out
 
 
@@ -399,6 +450,81 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
                     "hashes include the trials peers ran before the winner's hit reached them"}
 
 
+# Issue classes of one trial of K1's j-loop (4,831 VALU instructions, read from
+# the gfx950 ISA; tests/test_build.py checks these against the disassembly):
+# half rate = 2,046 v_alignbit_b32 + 726 v_add3_u32 + 9 otherwise full-rate ops
+# with an SGPR operand; full rate = v_bitop3_b32, v_add_u32, v_lshrrev_b32, ...
+TRIAL_HALF_RATE = 2781
+TRIAL_FULL_RATE = 2050
+
+
+def valu_peaks(miner, device: int, cu_count: int) -> dict:
+    """Measured ceilings (pow_valu_rate, include/pow_tools.h): the full-rate
+    chain (v_bitop3_b32 + v_add_u32, the SIMD-32 ceiling), the half-rate chain
+    (v_alignbit_b32 + v_add3_u32), the SHA mix, each with the clock the chip
+    held; and the mix-adjusted ceiling: K1's trial mix (TRIAL_*_RATE) issued at
+    the two isolated rates, priced at 5,000 algorithmic ops per hash."""
+    import ctypes
+
+    from mpi_blockchain_amd._lib import POW_VALU_FULL, POW_VALU_HALF, POW_VALU_MIX, ValuResult
+
+    out = {}
+    for name, kind in (("full_rate", POW_VALU_FULL), ("half_rate", POW_VALU_HALF), ("sha_mix", POW_VALU_MIX)):
+        r = ValuResult()
+        if miner.L.pow_valu_rate(device, kind, ctypes.byref(r)) == 0:
+            out[f"microbench_{name}"] = {"tops": round(r.lane_ops_per_s / 1e12, 2),
+                                         "clock_ghz": round(r.clock_hz / 1e9, 4),
+                                         "cycles_per_instr": round(r.cycles_per_instr, 3)}
+    f, h = out.get("microbench_full_rate"), out.get("microbench_half_rate")
+    if f and h:
+        hps = 1.0 / (TRIAL_HALF_RATE / (h["tops"] * 1e12) + TRIAL_FULL_RATE / (f["tops"] * 1e12))
+        out["mix_adjusted_ceiling_tops"] = round(hps * OPS_PER_HASH / 1e12, 2)
+        out["mix_adjusted_ceiling_hashes_per_s"] = round(hps, 1)
+        out["measured_clock_ghz"] = f["clock_ghz"]
+        out["peak_at_measured_clock_tops"] = round(cu_count * 4 * 32 * f["clock_ghz"] * 1e9 / 1e12, 2)
+    return out
+
+
+def roofline_block(achieved, kms, peak, live, traffic, traffic_source, algo_bytes, cu_count) -> dict:
+    """The roofline object of the bench line (int32 VALU issue bound)."""
+    r = {"bound": "valu_int32", "achieved": round(achieved, 3), "peak": peak["nominal_tops"],
+         "unit": "Tops/s", "frac": round(achieved / peak["nominal_tops"], 4),
+         "traffic": traffic, "algorithmic_bytes": algo_bytes, "ops_per_hash": OPS_PER_HASH,
+         "peak_detail": peak, "traffic_source": traffic_source,
+         "note": ("achieved = 2^32 hashes x 5000 int32 ops / mean HIP-event kernel time; peak = 256 CU x 4 SIMD "
+                  "x 32 lanes x nominal clock; traffic = FETCH_SIZE+WRITE_SIZE bytes per dispatch of the same "
+                  "workload")}
+    if "mix_adjusted_ceiling_tops" in peak:
+        r["frac_of_mix_adjusted_ceiling"] = round(achieved / peak["mix_adjusted_ceiling_tops"], 4)
+        r["frac_of_full_rate_microbench"] = round(achieved / peak["microbench_full_rate"]["tops"], 4)
+    if live is not None:
+        r["counters_live"] = live
+        v = live.get("valu", {})
+        if "clock_ghz" in v:
+            peak_clk = cu_count * 4 * 32 * v["clock_ghz"] * 1e9 / 1e12
+            r["valu_instr_per_hash"] = v["valu_instr_per_hash"]
+            r["valu_busy_pct"] = v["valu_busy_pct"]
+            r["cycles_per_valu_instr"] = v["cycles_per_valu_instr"]
+            r["measured_clock_ghz"] = v["clock_ghz"]
+            r["frac_at_measured_clock"] = round(achieved / peak_clk, 4)
+            # VALU lane-ops the counters saw issued, over the same kernel's duration in the pass
+            r["issued_frac_at_measured_clock"] = round(
+                v["counters"]["SQ_INSTS_VALU"] * 64 / (v["kernel_ns"] * 1e-9) / 1e12 / peak_clk, 4)
+    return r
+
+
+def list_fingerprint(buf, n: int) -> str:
+    """sha256 of the ascending solution list (little-endian u32), the form of
+    tests/golden/fingerprints_2p32*.json: the device list is copied once and
+    sorted on the host (after the timed region)."""
+    import hashlib
+
+    import numpy as np
+
+    a = np.sort(buf.read_u32(n))
+    return hashlib.sha256(a.astype("<u4").tobytes()).hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -435,14 +561,18 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
-    from mpi_blockchain_amd.shard import RcclGroup
+    from mpi_blockchain_amd.shard import RcclGroup, ShardedMiner
 
     miner = GpuMiner(local)
     rehearsal = os.environ.get("BENCH_REHEARSAL") == "1"
     # The library's own RCCL communicator (the id travels over torch.distributed);
-    # at N = 1 a one-rank group, used only by the group_search measurement.
+    # at N = 1 a one-rank group, used only by the group_search measurement.  A
+    # rehearsal (ranks sharing one GPU) runs the same pow_group rounds with the
+    # all-reduce over gloo (pow_group_init_custom): RCCL refuses two ranks on one GPU.
     group, group_err = None, None
-    if not rehearsal:
+    if rehearsal:
+        group = ShardedMiner(miner, rank, world)
+    else:
         try:
             group = RcclGroup.from_torch(miner) if dist is not None else \
                 RcclGroup(miner, 0, 1, RcclGroup.make_unique_id())
@@ -509,6 +639,8 @@ def main():
     # Per-rank parity (outside the timed region): every rank's window whose
     # fingerprints are committed (rank 0: [0, 2^32); rank 7: [7*2^32, 8*2^32),
     # the farthest window of an 8-GPU run) is checked against them.
+    n_loc = local_last[0][0]
+    local_last[0] = (*local_last[0], list_fingerprint(buf, n_loc) if d == 9 and n_loc <= cap else None)
     per_rank = [local_last[0]]
     if dist is not None:
         per_rank = [None] * world
@@ -537,7 +669,9 @@ def main():
     if do_proto:
         gone = wait_for_exit(pids[1:], timeout=120)
         proto = protocol_job(world) if gone else {"skipped": "bench ranks 1..N-1 did not exit within 120 s"}
-    collective = ("rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if group is not None and world > 1
+    collective = ("gloo all_reduce(min,sum) per step via pow_group_allreduce_u64 (pow_group_init_custom; "
+                  "rehearsal: ranks share one GPU)" if rehearsal and group is not None else
+                  "rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if group is not None and world > 1
                   else f"{dist.get_backend()} all_reduce(min,sum) per step via torch.distributed" if dist is not None
                   else "none (single process)")
 
@@ -546,24 +680,21 @@ def main():
     achieved = WINDOW * OPS_PER_HASH / (kms * 1e-3) / 1e12  # Tops/s of the dominant kernel
     clock_ghz = info["clock_khz"] / 1e6
     peak_nominal = info["cu_count"] * 4 * 32 * clock_ghz * 1e9 / 1e12  # SIMD-32: 128 lane-ops/CU/clk
-    peak = {"nominal_tops": round(peak_nominal, 2)}
+    peak = {"nominal_tops": round(peak_nominal, 2), "nominal_clock_ghz": clock_ghz, "cu_count": info["cu_count"]}
     if not args.no_peak:
-        import ctypes
-
-        lo, ms = ctypes.c_double(), ctypes.c_double()
-        if miner.L.pow_valu_peak(local, ctypes.byref(lo), ctypes.byref(ms)) == 0:
-            peak["microbench_tops"] = round(lo.value / 1e12, 2)
-    # HBM traffic of the dominant kernel: live rocprofv3 PMC passes at N = 1
-    # (a child process per pass, after the timed region); the committed summary
-    # of the same passes otherwise, labelled as such.
-    traffic, traffic_source, traffic_live = None, None, None
+        peak.update(valu_peaks(miner, local, info["cu_count"]))
+    # Counters of the dominant kernel: live rocprofv3 PMC passes at N = 1 (a
+    # child process per pass, after the timed region): HBM traffic, and the VALU
+    # instruction / busy / clock counters; the committed summary of the same
+    # traffic passes otherwise, labelled as such.
+    traffic, traffic_source, live = None, None, None
     if world == 1 and d == 9 and not args.no_pmc:
         try:
-            traffic_live = pmc_traffic_live()
+            live = pmc_live(info["cu_count"])
         except Exception as e:  # pragma: no cover - reported, not fatal
-            traffic_live = {"error": str(e)[-300:]}
-        if "total_bytes" in traffic_live:
-            traffic = traffic_live["total_bytes"]
+            live = {"error": str(e)[-300:]}
+        if "total_bytes" in live:
+            traffic = live["total_bytes"]
             traffic_source = ("measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes "
                               "(child processes, tools/ab_sweep over S0's 2^32 window at d = 9 with this build), "
                               "median per dispatch of 3")
@@ -574,16 +705,20 @@ def main():
     # sanity/parity at full size: rank 0's window is the golden 2^32 window
     parity = {"solutions_rank0": per_rank[0][0], "solutions_all_ranks": last[0], "lowest": last[1]}
     checked = {}
-    for r, (n_r, mn_r) in enumerate(per_rank):
+    for r, (n_r, mn_r, fp_r) in enumerate(per_rank):
         fpp = os.path.join(ROOT, "tests", "golden",
                            "fingerprints_2p32.json" if r == 0 else f"fingerprints_2p32_S0_at{r * WINDOW}.json")
         if d == 9 and os.path.exists(fpp):
             want = json.load(open(fpp))["ladder"]["9"]
             checked[str(r)] = {"solutions": n_r, "expected": want["count"],
-                               "ok": n_r == want["count"] and mn_r == r * WINDOW + want["first"][0]}
+                               "ok": n_r == want["count"] and mn_r == r * WINDOW + want["first"][0],
+                               "fingerprint_ok": fp_r == want["sha256_le_u32"]}
     if checked:
         parity["checked_ranks"] = checked
         parity["count_ok"] = all(c["ok"] for c in checked.values())
+        parity["fingerprint_ok"] = all(c["fingerprint_ok"] for c in checked.values())
+        parity["fingerprint"] = ("sha256 of each checked rank's sorted solution list (the timed step's device "
+                                 "output) vs tests/golden/fingerprints_2p32*.json")
     res = {
         "metric": "SHA-256 nonce trials/sec (whole job) + % int32 VALU peak",
         "value": round(value, 1),
@@ -603,13 +738,8 @@ def main():
                    "parallelism": f"static nonce shards x{world}; collective: {collective}"},
         "hashes_per_s_per_gpu": round(value / world, 1),
         "kernel_ms_per_step": round(kms, 3),
-        "roofline": {"bound": "valu_int32", "achieved": round(achieved, 3), "peak": peak["nominal_tops"],
-                     "unit": "Tops/s", "frac": round(achieved / peak["nominal_tops"], 4),
-                     "traffic": traffic, "algorithmic_bytes": 4 * (last[0] or 0),
-                     "ops_per_hash": OPS_PER_HASH, "peak_detail": peak,
-                     "traffic_source": traffic_source,
-                     "note": ("achieved = 2^32 hashes x 5000 int32 ops / mean HIP-event kernel time; "
-                              "traffic = FETCH_SIZE+WRITE_SIZE bytes per dispatch of the same workload")},
+        "roofline": roofline_block(achieved, kms, peak, live, traffic, traffic_source, 4 * (last[0] or 0),
+                                   info["cu_count"]),
         "device": info,
         "parity": parity,
     }
@@ -617,8 +747,6 @@ def main():
         res["cpu_baseline"] = cpu_baseline()
     if world == 1 and not args.no_ladder:
         res["ladder"] = ladder(miner)
-    if traffic_live is not None:
-        res["roofline"]["traffic_live"] = traffic_live
     if gsearch is not None:
         res["group_search"] = gsearch
     if group_err:

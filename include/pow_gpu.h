@@ -128,7 +128,12 @@ int pow_hash_block(pow_ctx* ctx, const pow_block* b, uint8_t digest[32], char he
  * the LOWEST solving counter in range and out->block_hash = its 64-char hex
  * digest + NUL (strcpy semantics of node.cpp:318: bytes 65..255 keep tmpl's);
  * *found_ctr = that counter.  Returns 0 if the range holds no solution or the
- * call was cancelled.  *hashes_done (optional) = trials issued. */
+ * call was cancelled.  *hashes_done (optional) = trials issued.
+ * pow_mine and pow_mine_any return as soon as the GPU has published the
+ * result; the ctx's stream may still be retiring the launch's last
+ * workgroup for a few microseconds (nothing it does then touches the result,
+ * the cancel word or a board, so unbinding or closing a board right away is
+ * safe).  The next launch on the ctx and pow_destroy are ordered behind it. */
 int pow_mine(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,
              unsigned diff_bits, const volatile uint32_t* cancel_word, uint32_t epoch,
              pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done);
@@ -192,8 +197,14 @@ int pow_dev_read(pow_ctx* ctx, const void* dev, void* host, size_t bytes);
  *     counters it would still compute (the lowest-counter result stays exact:
  *     counters below the peer's are always finished).
  * Such a call then returns 0 (the peer's result wins the caller's
- * reduction).  pow_group_* use a board automatically; these entry points are
- * for callers that drive several contexts themselves. */
+ * reduction).  In pow_mine that includes a call that found a solution while a
+ * peer already holds a lower one: the call's own counter is then not the
+ * search's answer, and not necessarily the lowest of its own range (its waves
+ * above the peer's counter may have stopped), so it is not reported.  A 1 from
+ * a bound pow_mine is the lowest solution of its range; the search's answer is
+ * the minimum over the ranks' results (pow_group_* reduce it for you).
+ * pow_group_* use a board automatically; these entry points are for callers
+ * that drive several contexts themselves. */
 #define POW_BOARD_MAX_SLOTS 64
 #define POW_BOARD_MAX_TAG 1023
 typedef struct pow_board pow_board;
@@ -237,6 +248,25 @@ int pow_group_unique_id(uint8_t id[POW_GROUP_ID_BYTES]);
 /* Joins the RCCL communicator on ctx's GPU; returns once all ranks joined. */
 int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
                    pow_group** out);
+/* The same group over a reduction the caller supplies instead of RCCL: the
+ * rounds, the stop board and the {counter, go, ok} consensus of
+ * pow_group_mine[_any] are unchanged, only the one all-reduce per round goes
+ * through `reduce`.  For ranks that already share a transport (MPI_Allreduce
+ * in an MPI job, torch.distributed gloo), and for several ranks on ONE GPU,
+ * which RCCL refuses (the multi-process GPU tests).  RCCL stays the
+ * collective of one process per GPU (pow_group_init).
+ *   reduce(user, vals, n, op): in place over every rank's n <= 8 words with
+ *       op = POW_REDUCE_*, collective (every rank calls it in the same order);
+ *       returns 0 on success.  Called from the thread that calls pow_group_*.
+ *   board_name: "/name" opens that node-local stop board (the same name on
+ *       every rank; fresh per group; unlinked once every rank has joined), or
+ *       NULL for none.
+ *   ctx may be NULL: the group then carries only pow_group_allreduce_u64.
+ * Collective: the first reduction (a barrier that also checks nranks) runs
+ * inside this call. */
+typedef int (*pow_group_reduce_fn)(void* user, uint64_t* vals, size_t n, int op);
+int pow_group_init_custom(pow_ctx* ctx, int nranks, int rank, pow_group_reduce_fn reduce, void* user,
+                          const char* board_name, pow_group** out);
 void pow_group_destroy(pow_group* g);
 /* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream. */
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);

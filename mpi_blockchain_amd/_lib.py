@@ -45,10 +45,24 @@ class Block(ctypes.Structure):
     ]
 
 
+# int reduce(void* user, uint64_t* vals, size_t n, int op): pow_group_reduce_fn
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
+                             ctypes.c_int)
+
+
 class PowStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("launches", ctypes.c_uint32),
                 ("hashes", ctypes.c_uint64)]
 
+
+class ValuResult(ctypes.Structure):
+    """pow_valu_result (include/pow_tools.h)."""
+
+    _fields_ = [("lane_ops_per_s", ctypes.c_double), ("kernel_ms", ctypes.c_double),
+                ("clock_hz", ctypes.c_double), ("cycles_per_instr", ctypes.c_double)]
+
+
+POW_VALU_MIX, POW_VALU_FULL, POW_VALU_HALF = 0, 1, 2
 
 assert ctypes.sizeof(Block) == 552
 
@@ -106,6 +120,8 @@ def load() -> ctypes.CDLL:
         "pow_group_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "pow_group_init": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                             ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "pow_group_init_custom": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, REDUCE_FN, ctypes.c_void_p,
+                                   ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "pow_group_destroy": ([ctypes.c_void_p], None),
         "pow_group_allreduce_u64": ([ctypes.c_void_p, c_u64p, ctypes.c_size_t, ctypes.c_int], ctypes.c_int),
         "pow_group_mine": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
@@ -120,6 +136,7 @@ def load() -> ctypes.CDLL:
         "pow_board_peek": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, c_u64p], ctypes.c_int),
         "pow_valu_peak": ([ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
                           ctypes.c_int),
+        "pow_valu_rate": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ValuResult)], ctypes.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -132,8 +149,8 @@ def load() -> ctypes.CDLL:
 EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_device_info",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
-           "pow_dev_read", "pow_valu_peak", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
-           "pow_group_destroy", "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",
+           "pow_dev_read", "pow_valu_peak", "pow_valu_rate", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
+           "pow_group_init_custom", "pow_group_destroy", "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",
            "pow_board_open", "pow_board_unlink", "pow_board_close", "pow_board_bind", "pow_board_post",
            "pow_board_peek")
 

@@ -58,6 +58,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
 MPI_HOME = os.environ.get("POW_MPI_HOME", "/opt/conda")  # the image's MPICH (mpi.h, libmpi.so)
 NODE_SRC = os.path.join(CSRC, "node", "pow_node.cpp")
 NODE_BIN = os.path.join(PKG, "bin", "pow_node")
+# The same node with the protocol tests' race-shaping switches compiled in
+# (-DPOW_NODE_TEST_KNOBS: --hold-first, --idle-below, --private-lead, pauses).
+# The shipped bin/pow_node behaves only as node.cpp does.
+NODE_TEST_BIN = os.path.join(PKG, "bin", "pow_node_test")
+NODE_TEST_KNOBS = ("--pause-ms", "--pause-us", "--winner-pause-us", "--hold-first", "--idle-below", "--private-lead")
 
 
 def mpi_available() -> bool:
@@ -65,30 +70,33 @@ def mpi_available() -> bool:
         os.path.exists(os.path.join(MPI_HOME, "lib", "libmpi.so"))
 
 
-def build_node(force: bool = False, verbose: bool = False) -> str | None:
+def build_node(force: bool = False, verbose: bool = False, test: bool = False) -> str | None:
     """The protocol node (C++ + MPI) over libpow_gpu.so; skipped without MPI.
+    test=True builds bin/pow_node_test (the test knobs compiled in).
     Run it with LD_LIBRARY_PATH=/lib/x86_64-linux-gnu:$MPI_HOME/lib (see
     mpi_blockchain_amd/node.py): MPICH's directory also holds an older
     libstdc++ that must not shadow the system one."""
     if not mpi_available():
         return None
     build(force=False, verbose=verbose)
+    out = NODE_TEST_BIN if test else NODE_BIN
     srcs = [NODE_SRC, LIB, os.path.join(ROOT, "include", "pow_gpu.h")]
-    if not force and os.path.exists(NODE_BIN) and \
-            all(os.path.getmtime(p) <= os.path.getmtime(NODE_BIN) for p in srcs):
-        return NODE_BIN
-    os.makedirs(os.path.dirname(NODE_BIN), exist_ok=True)
-    cmd = ["g++", "-std=c++17", "-O2", "-pthread", "-Wall", "-I", os.path.join(ROOT, "include"),
-           "-I", os.path.join(MPI_HOME, "include"), NODE_SRC, "-o", NODE_BIN + ".tmp",
+    if not force and os.path.exists(out) and all(os.path.getmtime(p) <= os.path.getmtime(out) for p in srcs):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O2", "-pthread", "-Wall", *(["-DPOW_NODE_TEST_KNOBS"] if test else []),
+           "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(MPI_HOME, "include"), NODE_SRC, "-o", out + ".tmp",
            "-L", PKG, "-lpow_gpu", "-Wl,-rpath,$ORIGIN/..",
            os.path.join(MPI_HOME, "lib", "libmpi.so"), f"-Wl,-rpath-link,{os.path.join(MPI_HOME, 'lib')}"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=ROOT)
-    os.replace(NODE_BIN + ".tmp", NODE_BIN)
-    return NODE_BIN
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_node(force="--force" in sys.argv, verbose=True))
+    print(build_node(force="--force" in sys.argv, verbose=True, test=True))

@@ -38,8 +38,13 @@
 // set-up then runs BEFORE MPI_Init, and MPI_Init is the start line, as in the
 // reference.
 //
-//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--pause-ms MS | --pause-us US]
-//            [--winner-pause-us US] [--serial-init 0|1] [--hold-first 0|1] [--idle-below K]
+//   pow_node [--difficulty D] [--blocks N] [--device G] [--round LOG2] [--serial-init 0|1]
+//
+// Test knobs.  bin/pow_node behaves only as node.cpp does.  The race-shaping
+// switches the protocol tests need are compiled only into bin/pow_node_test
+// (-DPOW_NODE_TEST_KNOBS, mpi_blockchain_amd/build.py):
+//            [--pause-ms MS | --pause-us US] [--winner-pause-us US] [--hold-first 0|1]
+//            [--idle-below K] [--private-lead K]
 #include <mpi.h>
 #include <unistd.h>
 
@@ -72,21 +77,34 @@ constexpr int kTagNewBlock = 10;
 constexpr int kTagChainHash = 21;
 constexpr int kTagChainResponse = 22;
 
+#ifdef POW_NODE_TEST_KNOBS
+// Race shaping for the protocol tests (bin/pow_node_test only).
+struct TestKnobs {
+  unsigned winner_pause_us = 0;  // sleep after mining a block (GPU blocks take ~35 us, so the last
+                                 // finder would otherwise start every race first)
+  unsigned pause_us = 0;         // sleep a random 0..pause_us us before each round (lets slower CPU
+                                 // ranks compete, and decorrelates GPU ranks so forks happen)
+  bool hold_first = false;       // every rank mines block 1, then all publish it after one
+                                 // MPI_Barrier, so every rank receives a rival block 1 (a certain fork)
+  unsigned idle_below = 0;       // do not mine while the chain is below this index (the blocks
+                                 // before it come from other ranks, e.g. the reference's CPU ranks)
+  unsigned private_lead = 0;     // K >= 2: every rank mines blocks 1..K on a private branch, then all
+                                 // publish their tips after one barrier: each receiver is K behind
+                                 // and asks the tip's owner for its chain while that owner asks it
+                                 // (the mutual request node.cpp:155-161, 404-405 deadlocks on)
+};
+#endif
+
 struct Options {
   unsigned difficulty = 9;  // DEFAULT_DIFFICULTY (block.h:6)
   unsigned blocks = 10;     // BLOCKS_TO_MINE (block.h:7)
   int device = -1;          // -1: local rank modulo visible GPUs
   unsigned round_log2 = 32; // counters per pow_mine call
-  unsigned winner_pause_us = 0;  // tests: sleep after mining a block (GPU blocks take ~35 us, so
-                                // the last finder would otherwise start every race first)
-  unsigned pause_us = 0;    // sleep a random 0..pause_us us before each round (tests: lets slower
-                            // CPU ranks compete, and decorrelates GPU ranks so forks happen)
   bool serial_init = false; // --serial-init 1: GPU set-up before MPI_Init instead of beside it
                             // (and no start barrier: mixed jobs with reference ranks)
-  bool hold_first = false;  // tests: every rank mines block 1, then all publish it after one
-                            // MPI_Barrier, so every rank receives a rival block 1 (a certain fork)
-  unsigned idle_below = 0;  // tests: do not mine while the chain is below this index (the blocks
-                            // before it come from other ranks, e.g. the reference's CPU ranks)
+#ifdef POW_NODE_TEST_KNOBS
+  TestKnobs t;
+#endif
 };
 
 // MPI_Probe that sleeps between polls instead of spinning.  MPICH's blocking
@@ -132,7 +150,11 @@ class Node {
   pow_ctx* mine_ctx_ = nullptr;              // used only by the mining thread
   pow_ctx* recv_ctx_ = nullptr;              // used only by the receive thread
   std::deque<std::pair<pow_block, MPI_Status>> deferred_;
+#ifdef POW_NODE_TEST_KNOBS
   std::atomic<int> rivals1_{0};  // --hold-first: peers' blocks 1 this rank has processed
+  MPI_Comm test_comm_ = MPI_COMM_NULL;  // --private-lead: the receive thread's own barrier
+  bool tip_seen_ = false;               // --private-lead: a peer's private tip has arrived
+#endif
 
   // The chain moved: a running pow_mine_any on the old template stops at its
   // next GPU poll (pow_cancel), not at its next sub-round (up to ~0.13 s).
@@ -252,6 +274,12 @@ class Node {
       MPI_Recv(&buf, 1, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);
       if (st.MPI_TAG == kTagChainHash) {
         printf("[%u] TAG_CHAIN_HASH \n", rank_);
+#ifdef POW_NODE_TEST_KNOBS
+        // the case the hardening is for: a chain request served while this
+        // rank itself waits for a TAG_CHAIN_RESPONSE (the reference blocks in
+        // MPI_Recv here, holding the mutex its receive loop needs)
+        printf("[%d] TAG_CHAIN_HASH de %d atendido mientras espero la cadena de %d \n", rank_, st.MPI_SOURCE, owner);
+#endif
         send_blockchain(buf, st.MPI_SOURCE);
       } else if (st.MPI_TAG == kTagNewBlock) {
         deferred_.emplace_back(buf, st);
@@ -339,9 +367,61 @@ class Node {
   }
 
   // node.cpp:278-332 with node.cpp:302-308 on the GPU.
+#ifdef POW_NODE_TEST_KNOBS
+  // --private-lead K: mine blocks 1..K on a private branch (inserted into
+  // node_blocks so send_blockchain can serve them, but never adopted as
+  // last_block_in_chain), then publish only the tip after one barrier, outside
+  // the mutex, so every rank's tip goes out at once.  Each receiver is K
+  // behind ("Perdí la carrera por varios", node.cpp:249-253) and asks the
+  // tip's owner for its chain while that owner asks it.  Then wait (bounded)
+  // until this rank has migrated, so no block 1 is mined on genesis meanwhile.
+  void private_lead(std::mt19937_64& rng, uint64_t round) {
+    pow_block prev;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      prev = *last_;
+    }
+    for (unsigned k = 0; k < opt_.t.private_lead;) {
+      pow_block tmpl = prev, solved;
+      tmpl.index += 1;
+      tmpl.node_owner_number = (uint32_t)rank_;
+      tmpl.difficulty = opt_.difficulty;
+      tmpl.created_at = (uint64_t)time(nullptr);
+      memcpy(tmpl.previous_block_hash, prev.block_hash, POW_HASH_SIZE);
+      uint64_t ctr = 0;
+      const int rc = pow_mine_any(mine_ctx_, &tmpl, rng() % (POW_COUNTER_LIMIT - round), round, opt_.difficulty,
+                                  nullptr, 0, &solved, &ctr, nullptr);
+      if (rc < 0) {
+        fprintf(stderr, "[%d] pow_mine_any: %s\n", rank_, pow_last_error());
+        MPI_Abort(MPI_COMM_WORLD, 1);
+      }
+      if (rc != 1) continue;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        blocks_.insert({hash_of(solved), solved});
+      }
+      printf("[%d] Bloque privado con index %u \n", rank_, solved.index);
+      prev = solved;
+      ++k;
+    }
+    MPI_Barrier(MPI_COMM_WORLD);
+    send_block_to_everyone(prev);
+    for (int w = 0; w < 40000; ++w) {
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (last_->index >= opt_.t.private_lead) break;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+#endif
+
   void proof_of_work() {
     std::mt19937_64 rng((uint64_t)time(nullptr) + (uint64_t)rank_);  // node.cpp:386
     const uint64_t round = 1ull << opt_.round_log2;
+#ifdef POW_NODE_TEST_KNOBS
+    if (opt_.t.private_lead >= 2) private_lead(rng, round);
+#endif
     for (;;) {
       pow_block tmpl;
       uint32_t ep;
@@ -355,17 +435,21 @@ class Node {
         tmpl = *last_;
         ep = __atomic_load_n(&epoch_, __ATOMIC_SEQ_CST);
       }
-      if (tmpl.index < opt_.idle_below) {  // --idle-below: only receive for now
+#ifdef POW_NODE_TEST_KNOBS
+      if (tmpl.index < opt_.t.idle_below) {  // --idle-below: only receive for now
         std::this_thread::sleep_for(std::chrono::microseconds(200));
         continue;
       }
+#endif
       // node.cpp:295-299
       tmpl.index += 1;
       tmpl.node_owner_number = (uint32_t)rank_;
       tmpl.difficulty = opt_.difficulty;
       tmpl.created_at = (uint64_t)time(nullptr);
       memcpy(tmpl.previous_block_hash, tmpl.block_hash, POW_HASH_SIZE);
-      if (opt_.pause_us) std::this_thread::sleep_for(std::chrono::microseconds(rng() % (opt_.pause_us + 1ull)));
+#ifdef POW_NODE_TEST_KNOBS
+      if (opt_.t.pause_us) std::this_thread::sleep_for(std::chrono::microseconds(rng() % (opt_.t.pause_us + 1ull)));
+#endif
       const uint64_t start = rng() % (POW_COUNTER_LIMIT - round);
       pow_block solved;
       uint64_t ctr = 0;
@@ -375,7 +459,8 @@ class Node {
         fprintf(stderr, "[%d] pow_mine_any: %s\n", rank_, pow_last_error());
         MPI_Abort(MPI_COMM_WORLD, 1);
       }
-      if (rc == 1 && opt_.hold_first && solved.index == 1) {
+#ifdef POW_NODE_TEST_KNOBS
+      if (rc == 1 && opt_.t.hold_first && solved.index == 1) {
         // --hold-first: adopt block 1, wait until every rank has mined its
         // own block 1, then publish.  Each rank then receives rival blocks 1
         // while its chain is at index 1: "Conflicto de branch" (node.cpp:235)
@@ -404,7 +489,10 @@ class Node {
         // not hold the network up past 2 s.
         for (int w = 0; w < 40000 && rivals1_.load(std::memory_order_acquire) < size_ - 1; ++w)
           std::this_thread::sleep_for(std::chrono::microseconds(50));
-      } else if (rc == 1) {  // node.cpp:311-327
+        continue;
+      }
+#endif
+      if (rc == 1) {  // node.cpp:311-327
         std::lock_guard<std::mutex> g(mu_);
         if (last_->index < solved.index) {
           const std::string h = hash_of(solved);
@@ -414,9 +502,11 @@ class Node {
           send_block_to_everyone(*last_);
         }
       }
+#ifdef POW_NODE_TEST_KNOBS
       // Tests: let the other ranks receive this block before racing on the next.
-      if (rc == 1 && opt_.winner_pause_us)
-        std::this_thread::sleep_for(std::chrono::microseconds(opt_.winner_pause_us));
+      if (rc == 1 && opt_.t.winner_pause_us)
+        std::this_thread::sleep_for(std::chrono::microseconds(opt_.t.winner_pause_us));
+#endif
     }
     MPI_Abort(MPI_COMM_WORLD, 0);  // node.cpp:330
   }
@@ -451,6 +541,9 @@ int Node::run() {
   MPI_Comm_size(MPI_COMM_WORLD, &size_);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank_);
   define_block_type();
+#ifdef POW_NODE_TEST_KNOBS
+  if (opt_.t.private_lead >= 2) MPI_Comm_dup(MPI_COMM_WORLD, &test_comm_);
+#endif
   printf("[MPI] Lanzando proceso %u\n", rank_);
   std::remove((std::to_string(rank_) + ".out").c_str());  // blockchain.cpp:31 does `rm *.out`
 
@@ -483,10 +576,21 @@ int Node::run() {
       }
       MPI_Recv(&buf, 1, block_type_, st.MPI_SOURCE, st.MPI_TAG, MPI_COMM_WORLD, &st);
     }
+#ifdef POW_NODE_TEST_KNOBS
+    // --private-lead: every receive thread holds its first peer tip until all
+    // have one, so all ranks enter verificar_y_migrar_cadena together and each
+    // one's TAG_CHAIN_HASH reaches a rank that is itself waiting for a chain.
+    if (opt_.t.private_lead >= 2 && !tip_seen_ && st.MPI_TAG == kTagNewBlock && buf.index == opt_.t.private_lead) {
+      tip_seen_ = true;
+      MPI_Barrier(test_comm_);
+    }
+#endif
     std::lock_guard<std::mutex> g(mu_);
     if (st.MPI_TAG == kTagNewBlock) {
       validate_block_for_chain(buf, st);
+#ifdef POW_NODE_TEST_KNOBS
       if (buf.index == 1) rivals1_.fetch_add(1, std::memory_order_release);
+#endif
     } else if (st.MPI_TAG == kTagChainHash) {
       printf("[%u] TAG_CHAIN_HASH \n", rank_);
       send_blockchain(buf, st.MPI_SOURCE);
@@ -507,12 +611,19 @@ int main(int argc, char** argv) {
     else if (k == "--blocks") o.blocks = (unsigned)v;
     else if (k == "--device") o.device = (int)v;
     else if (k == "--round") o.round_log2 = (unsigned)std::min(40l, std::max(12l, v));
-    else if (k == "--pause-ms") o.pause_us = (unsigned)v * 1000u;
-    else if (k == "--pause-us") o.pause_us = (unsigned)v;
-    else if (k == "--winner-pause-us") o.winner_pause_us = (unsigned)v;
     else if (k == "--serial-init") o.serial_init = v != 0;
-    else if (k == "--hold-first") o.hold_first = v != 0;
-    else if (k == "--idle-below") o.idle_below = (unsigned)std::max(0l, v);
+#ifdef POW_NODE_TEST_KNOBS
+    else if (k == "--pause-ms") o.t.pause_us = (unsigned)v * 1000u;
+    else if (k == "--pause-us") o.t.pause_us = (unsigned)v;
+    else if (k == "--winner-pause-us") o.t.winner_pause_us = (unsigned)v;
+    else if (k == "--hold-first") o.t.hold_first = v != 0;
+    else if (k == "--idle-below") o.t.idle_below = (unsigned)std::max(0l, v);
+    else if (k == "--private-lead") o.t.private_lead = (unsigned)std::min(5l, std::max(0l, v));  // <= VALIDATION_BLOCKS
+#endif
+    else {
+      fprintf(stderr, "pow_node: unknown option %s (race-shaping test knobs are in pow_node_test)\n", k.c_str());
+      return 2;
+    }
   }
   Node n(o);
   int gpu_rc = 0;

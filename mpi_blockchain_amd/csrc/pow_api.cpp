@@ -208,6 +208,7 @@ struct pow_ctx {
   size_t hash_cap = 0;
   unsigned grid_full = 0;  // workgroups that fill the chip (8 per CU)
   bool force_full = false; // POW_FORCE_FULL=1: use the d > 32 kernel for every d (tests)
+  bool fault_mine = false;  // POW_FAULT_INJECT=mine: every pow_mine[_any] call fails (failure-propagation tests)
   uint64_t lat_max = 1ull << 24;  // POW_LAT_MAX: first-sub-round cap for K1' (0 = K1 only)
   unsigned lat_wps = 0;           // POW_LAT_WPS (tuning runs): K1' waves per SIMD at every d (0 = plan)
   pow_stats stats{};
@@ -473,6 +474,7 @@ int pow_init(int device, pow_ctx** out) {
   // can run beside a K1 launch instead of waiting up to its whole ~0.13 s.
   ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u - 1u;
   if (const char* ff = getenv("POW_FORCE_FULL")) ctx->force_full = ff[0] == '1';
+  if (const char* fi = getenv("POW_FAULT_INJECT")) ctx->fault_mine = std::strcmp(fi, "mine") == 0;
   if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
   if (const char* lw = getenv("POW_LAT_WPS")) ctx->lat_wps = (unsigned)std::min(8ul, strtoul(lw, nullptr, 0));
   if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
@@ -740,6 +742,7 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   if (int rc = set_dev(ctx)) return rc;
   ctx->stats = pow_stats{};
   if (hashes_done) *hashes_done = 0;
+  if (ctx->fault_mine) return fail(POW_EHIP, "injected fault (POW_FAULT_INJECT=mine)");
   if (int rc = upload_consts(ctx, tmpl)) return rc;
   ctx->launch_epoch = epoch;
   ctx->watch_epoch = cancel_word != nullptr;
@@ -796,6 +799,11 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
         if (any ? (!h || c->rel < h->rel) : c->rel == r.min_rel) h = c;
       }
       const uint64_t ctr = s0 + (h ? h->rel : r.min_rel);
+      // Lowest mode with a bound board: a peer already holds a lower counter,
+      // so this one is not the search's answer (and, since waves between the
+      // peer's counter and this one may have stopped early, not necessarily
+      // the lowest of this call's range either): the peer's result wins.
+      if (!any && board_peer_min(ctx) < ctr) break;
       *out = *tmpl;
       pow_nonce_from_counter(ctr, out->nonce);
       char hx[65];

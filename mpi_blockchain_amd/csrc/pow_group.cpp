@@ -22,7 +22,10 @@
 // winner the ranks already know of.
 //
 // RCCL is opened with dlopen at first use, so libpow_gpu.so has no link-time
-// dependency on it and the single-GPU entry points never load it.
+// dependency on it and the single-GPU entry points never load it.  A group
+// made by pow_group_init_custom runs the same rounds over the caller's
+// reduction instead (MPI_Allreduce, torch.distributed, or several test ranks
+// sharing one GPU, which RCCL refuses).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -86,9 +89,11 @@ constexpr size_t kMaxWords = 8;
 }  // namespace
 
 struct pow_group {
-  pow_ctx* ctx = nullptr;
+  pow_ctx* ctx = nullptr;     // null: a group that only carries collectives (pow_group_init_custom)
   int nranks = 1, rank = 0;
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;  // RCCL communicator (pow_group_init) ...
+  pow_group_reduce_fn reduce = nullptr;  // ... or the caller's reduction (pow_group_init_custom)
+  void* reduce_user = nullptr;
   uint64_t* d_buf = nullptr;  // kMaxWords device words: the all-reduce operand
   uint64_t* h_buf = nullptr;  // pinned host mirror
   pow_board* board = nullptr; // the node's stop board (null: more than 64 ranks, or none available)
@@ -97,15 +102,21 @@ struct pow_group {
 
 namespace {
 
-// In-place all-reduce of n <= kMaxWords u64 on the ctx's stream.
-int group_allreduce(pow_group* g, uint64_t* v, size_t n, ncclRedOp_t op) {
+// In-place all-reduce of n <= kMaxWords u64 (op = POW_REDUCE_*): RCCL on the
+// ctx's stream, or the caller's reduction of a custom group.
+int group_allreduce(pow_group* g, uint64_t* v, size_t n, int op) {
+  if (g->reduce) {
+    if (g->reduce(g->reduce_user, v, n, op) != 0) return pow_set_error(POW_ECOMM, "custom reduction failed");
+    return POW_OK;
+  }
+  const ncclRedOp_t o = op == POW_REDUCE_MIN ? ncclMin : op == POW_REDUCE_MAX ? ncclMax : ncclSum;
   hipError_t e = hipSetDevice(pow_ctx_device(g->ctx));
   if (e != hipSuccess) return hip_fail("hipSetDevice", e);
   hipStream_t st = (hipStream_t)pow_ctx_stream(g->ctx);
   memcpy(g->h_buf, v, n * sizeof(uint64_t));
   if ((e = hipMemcpyAsync(g->d_buf, g->h_buf, n * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
     return hip_fail("hipMemcpyAsync", e);
-  ncclResult_t r = rccl().all_reduce(g->d_buf, g->d_buf, n, ncclUint64, op, g->comm, st);
+  ncclResult_t r = rccl().all_reduce(g->d_buf, g->d_buf, n, ncclUint64, o, g->comm, st);
   if (r != ncclSuccess) return comm_fail("ncclAllReduce", r);
   if ((e = hipMemcpyAsync(g->h_buf, g->d_buf, n * 8, hipMemcpyDeviceToHost, st)) != hipSuccess)
     return hip_fail("hipMemcpyAsync", e);
@@ -185,7 +196,7 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
       }
     }
     if (cancel_moved(cancel_word, epoch)) v[1] = 0;
-    if (int rc = group_allreduce(g, v, 3, ncclMin)) return rc;
+    if (int rc = group_allreduce(g, v, 3, POW_REDUCE_MIN)) return rc;
     if (hashes_done) *hashes_done = st.s.hashes;
     pow_ctx_set_stats(g->ctx, st.s);
     if (v[2] == 0)  // every rank leaves the search together
@@ -207,6 +218,7 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
 int check_args(const pow_group* g, const pow_block* tmpl, const pow_block* out, uint64_t ctr_start,
                uint64_t ctr_count, unsigned diff_bits) {
   if (!g || !tmpl || !out) return pow_set_error(POW_EINVAL, "null");
+  if (!g->ctx) return pow_set_error(POW_EINVAL, "group has no context (collectives only)");
   if (ctr_start >= POW_COUNTER_LIMIT || ctr_count > POW_COUNTER_LIMIT - ctr_start)
     return pow_set_error(POW_EINVAL, "counter range past 62^9");
   if (diff_bits > 256) return pow_set_error(POW_EINVAL, "difficulty > 256 bits");
@@ -277,13 +289,45 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
   return POW_OK;
 }
 
+int pow_group_init_custom(pow_ctx* ctx, int nranks, int rank, pow_group_reduce_fn reduce, void* user,
+                          const char* board_name, pow_group** out) {
+  if (!out) return pow_set_error(POW_EINVAL, "null out");
+  *out = nullptr;
+  if (!reduce) return pow_set_error(POW_EINVAL, "null reduction");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return pow_set_error(POW_EINVAL, "bad rank/nranks");
+  pow_group* g = new pow_group;
+  g->ctx = ctx;
+  g->nranks = nranks;
+  g->rank = rank;
+  g->reduce = reduce;
+  g->reduce_user = user;
+  // As pow_group_init: every rank opens the board before the first
+  // collective, which doubles as the barrier after which the name can go.
+  if (board_name && ctx && nranks <= POW_BOARD_MAX_SLOTS && pow_board_open(board_name, nranks, &g->board) != POW_OK)
+    g->board = nullptr;
+  uint64_t joined = 1;
+  const int rc = group_allreduce(g, &joined, 1, POW_REDUCE_SUM);
+  if (board_name && ctx) pow_board_unlink(board_name);
+  if (rc != POW_OK || joined != (uint64_t)nranks) {
+    pow_group_destroy(g);
+    if (rc != POW_OK) return rc;
+    char msg[128];
+    snprintf(msg, sizeof msg, "%llu ranks joined a group of %d", (unsigned long long)joined, nranks);
+    return pow_set_error(POW_ECOMM, msg);
+  }
+  *out = g;
+  return POW_OK;
+}
+
 void pow_group_destroy(pow_group* g) {
   if (!g) return;
-  (void)hipSetDevice(pow_ctx_device(g->ctx));
+  if (g->ctx) {
+    (void)hipSetDevice(pow_ctx_device(g->ctx));
+    pow_board_bind(g->ctx, nullptr, 0, 0);
+  }
   if (g->comm) (void)rccl().comm_destroy(g->comm);
-  pow_board_bind(g->ctx, nullptr, 0, 0);
   pow_board_close(g->board);
-  (void)hipFree(g->d_buf);
+  if (g->d_buf) (void)hipFree(g->d_buf);
   if (g->h_buf) (void)hipHostFree(g->h_buf);
   delete g;
 }
@@ -291,13 +335,10 @@ void pow_group_destroy(pow_group* g) {
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op) {
   if (!g || (n && !vals)) return pow_set_error(POW_EINVAL, "null");
   if (n > kMaxWords) return pow_set_error(POW_EINVAL, "at most 8 words per all-reduce");
-  ncclRedOp_t o;
-  if (op == POW_REDUCE_MIN) o = ncclMin;
-  else if (op == POW_REDUCE_MAX) o = ncclMax;
-  else if (op == POW_REDUCE_SUM) o = ncclSum;
-  else return pow_set_error(POW_EINVAL, "unknown reduction");
+  if (op != POW_REDUCE_MIN && op != POW_REDUCE_MAX && op != POW_REDUCE_SUM)
+    return pow_set_error(POW_EINVAL, "unknown reduction");
   if (n == 0) return POW_OK;
-  return group_allreduce(g, vals, n, o);
+  return group_allreduce(g, vals, n, op);
 }
 
 int pow_group_mine(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64_t ctr_count,

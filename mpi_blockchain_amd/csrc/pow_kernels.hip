@@ -162,9 +162,11 @@ __device__ __forceinline__ bool poll_stop(const PowWatch& w, unsigned int* cance
 
 // A hit of a mine launch goes to this context's board slot at once (system
 // scope, straight into host memory), so the peers' sentinels see it within
-// their next poll.  Several lanes may store: any stored value is a real
-// solution, and a peer only ever compares against it (a higher value than
-// this launch's lowest just stops the peers a little less eagerly).
+// their next poll.  Only a lane whose atomicMin lowered the launch's minimum
+// stores (the callers below), so the slot's value only falls, except in the
+// rare race of two lowering lanes whose stores land out of order; the host
+// posts the call's exact result when it returns.  Any stored value is a real
+// solution, and a peer only ever compares against it.
 __device__ __forceinline__ void publish_hit(const PowWatch& w, unsigned long long rel) {
   unsigned long long* const mine = w.board_mine;
   if (mine)
@@ -211,6 +213,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
   // chunks 1-4's K+W words, one per thread (blockDim = 256 = 4 x 64)
   __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
   lkw[threadIdx.x] = (&C->kw[0][0])[threadIdx.x];
+  __shared__ uint32_t sibs_done;  // mine modes, workgroup 0: waves 1..3 that have finished (see the exit)
+  if (threadIdx.x == 0) sibs_done = 0;
   __syncthreads();
 
   for (;;) {
@@ -364,10 +368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         if (__builtin_expect(hit, 0)) {
           const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
           // rel < count also rejects j < off0 at r = 0 (wraps) and lanes past the end
-          if (rel < L.count) {
-            atomicMin(&res->min_rel, rel);
-            publish_hit(res->watch, rel);
-          }
+          if (rel < L.count && rel < atomicMin(&res->min_rel, rel)) publish_hit(res->watch, rel);
         }
       } else {
         bool ok = false;
@@ -402,15 +403,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
     if (lane == 0 && mymin != ~0ull) atomicMin(&res->min_rel, mymin);
   }
   if (MODE >= 1) {
+    // The sentinel (workgroup 0, wave 0) is the only reader of host memory
+    // (poll_stop).  It must outlive every other wave of the launch: once it
+    // leaves, the waves still finishing their last chunks would miss a
+    // pow_cancel or a peer's hit (up to ~1 chunk, ~4 ms).  So it keeps
+    // polling, with s_sleep between polls, until its three siblings are done
+    // and every other workgroup has counted its exit.  Every other wave has
+    // finite work (and a workgroup that starts late finds the queue empty),
+    // so the wait ends.
+    if (blockIdx.x == 0) {
+      if (threadIdx.x >= 64u) {
+        if (lane == 0) __hip_atomic_fetch_add(&sibs_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (res->watch.watch_epoch || res->watch.board) {
+        for (;;) {
+          const uint32_t sd = __hip_atomic_load(&sibs_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t ex = __hip_atomic_load(&res->wg_exits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__builtin_amdgcn_readfirstlane(sd) >= (blockDim.x >> 6) - 1u &&
+              __builtin_amdgcn_readfirstlane(ex) >= gridDim.x - 1u)
+            break;
+          (void)poll_stop(res->watch, &res->cancelled, &res->peer_abs, ~0ull);
+          __builtin_amdgcn_s_sleep(32);
+        }
+      }
+    }
     // Trials computed (lanes of a wave run the same iterations), summed per
     // workgroup first: after a hit in MODE 2 all ~8,000 waves exit within one
     // step, and one atomic each on the same address would queue for tens of us.
     __shared__ uint32_t wave_iters[4];
     if ((threadIdx.x & 63u) == 0) wave_iters[threadIdx.x >> 6] = iters;
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
       atomicAdd(&res->hashes,
                 (unsigned long long)(wave_iters[0] + wave_iters[1] + wave_iters[2] + wave_iters[3]) * 64ull);
+      if (blockIdx.x != 0) atomicAdd(&res->wg_exits, 1u);
+    }
   }
 }
 
@@ -540,8 +566,7 @@ __global__ __launch_bounds__(256) void pow_search_lat(
     bool hit = D[0] <= L.thr;
     if (FULL && hit) hit = full_test(D, L.diff);
     if (__builtin_expect(hit, 0) && (unsigned long long)rel < L.count) {
-      atomicMin(&res->min_rel, (unsigned long long)rel);
-      publish_hit(L.watch, rel);
+      if ((unsigned long long)rel < atomicMin(&res->min_rel, (unsigned long long)rel)) publish_hit(L.watch, rel);
       const uint32_t slot = atomicAdd(&res->nhit, 1u);
       if (slot < POW_HITS) {
         res->hit[slot].rel = rel;

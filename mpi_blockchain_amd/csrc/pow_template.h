@@ -130,7 +130,8 @@ struct PowResult {
   unsigned long long count;    // sweep: solutions in the main list (32-entry blocks); 64-bit, since
                                // at d = 0 a 2^32 window has 2^32 solutions
   unsigned int next;           // next prefix chunk to hand out (dynamic work queue)
-  unsigned int pad0;
+  unsigned int wg_exits;       // K1 mine modes: workgroups other than 0 that have exited (the
+                               // sentinel wave of workgroup 0 polls host memory until all have)
   unsigned int tail;           // sweep: solutions in tail_buf (< 32 per wave)
   unsigned int tail_cap;       // entries of tail_buf
   unsigned int* tail_buf;      // sweep: each wave's last < 32 solutions (appended by the host);

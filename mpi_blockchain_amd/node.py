@@ -13,7 +13,7 @@ import re
 import subprocess
 from dataclasses import dataclass, field
 
-from .build import MPI_HOME, NODE_BIN, build_node
+from .build import MPI_HOME, NODE_TEST_KNOBS, build_node
 
 MPIEXEC = os.path.join(MPI_HOME, "bin", "mpiexec")
 
@@ -73,8 +73,10 @@ def chain_status(entries: list[ChainEntry], blocks: int, difficulty: int) -> tup
 
 def run_network(n_gpu: int, workdir: str, difficulty: int = 9, blocks: int = 10, timeout: float = 240,
                 ref_binary: str | None = None, n_ref: int = 0, extra_args=()) -> NetworkRun:
-    """mpiexec with n_ref reference ranks (if given) followed by n_gpu GPU ranks."""
-    node = build_node()
+    """mpiexec with n_ref reference ranks (if given) followed by n_gpu GPU ranks.
+    Runs bin/pow_node, or bin/pow_node_test when `extra_args` hold one of the
+    protocol tests' race-shaping knobs (build.NODE_TEST_KNOBS)."""
+    node = build_node(test=any(str(a) in NODE_TEST_KNOBS for a in extra_args))
     if node is None:
         raise RuntimeError("MPI (mpi.h / libmpi.so) not found: cannot build the protocol node")
     args = [node, "--difficulty", str(difficulty), "--blocks", str(blocks), *map(str, extra_args)]

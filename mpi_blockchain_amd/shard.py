@@ -1,95 +1,111 @@
 """Nonce space sharded over GPUs, winner chosen by an all-reduce(min).
 
-BASELINE config 4: one process per GPU (``torch.distributed``, backend
-``nccl`` = RCCL over xGMI on ROCm).  Every search round R counters wide is cut
-into ``world`` contiguous static shards; each rank mines the LOWEST solving
-counter of its shard on its own GPU (``pow_mine``), then one 8-byte
-``all_reduce(MIN)`` picks the global winner — the same counter a single GPU (or
-the CPU oracle) finds first, so the result is deterministic.  A non-empty
-result ends the search on every rank (cancellation).  There is no data-path
-collective: the only exchange is the 8-byte min per round.
+BASELINE config 4: one process per GPU.  Every search round is cut into
+``world`` contiguous static shards; each rank mines its shard on its own GPU,
+then ONE 24-byte all-reduce(MIN) of {counter found, go, ok} picks the winner
+(the same counter a single GPU, or the CPU oracle, finds first in lowest
+mode), spreads cancellation and reports a failed rank.  Inside a round the
+ranks of one node also share a stop board, so the finder stops the other
+GPUs' running kernels.  There is no data-path collective.
+
+The search itself is implemented once, in C++ (``pow_group_*`` of
+libpow_gpu.so, mpi_blockchain_amd/csrc/pow_group.cpp).  This module only
+builds the group:
+
+* :class:`RcclGroup` — the product path: RCCL (``ncclAllReduce``) called from
+  C++, one process per GPU (bench.py at N > 1).
+* :class:`ShardedMiner` — the same C++ rounds over torch.distributed's
+  collectives (``pow_group_init_custom``): gloo on CPU, or several ranks that
+  share one GPU (the multi-process GPU tests, bench.py's rehearsal), which
+  RCCL refuses.
 
 The reference has no mining-side collective (each MPI rank mines its own
-template with its own rand() stream, node.cpp:386); this is the MI355X-native
-replacement for "all ranks search, first solution wins".
+template with its own rand() stream, node.cpp:302, 386); this is the
+MI355X-native replacement for "all ranks search, first solution wins".
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Callable, Optional
+import os
+import uuid
 
-NONE = (1 << 63) - 1  # "no solution" in the int64 all-reduce
+from ._lib import POW_REDUCE_MAX, POW_REDUCE_MIN, POW_REDUCE_SUM, REDUCE_FN, Block, check, load
+
+_U64 = 1 << 64
+_HALF = 1 << 63
 
 
 def partition(start: int, count: int, rank: int, world: int) -> tuple[int, int]:
-    """Contiguous static shard of [start, start+count) for `rank`."""
+    """Contiguous static shard of [start, start+count) for `rank`
+    (the Python mirror of pow_group_partition, tested equal)."""
     base, extra = divmod(count, world)
     lo = start + rank * base + min(rank, extra)
     return lo, base + (1 if rank < extra else 0)
 
 
-def round_plan(world: int, difficulty: int) -> tuple[int, int]:
-    """First round size and cap of the adaptive plan (as pow_group_mine):
-    ~4x the expected trials, at least 2^16 per rank; rounds then grow 4x up
-    to 2^30 per rank."""
-    big = world << 30
-    return min(big, max(world << 16, 1 << (min(difficulty, 40) + 2))), big
+def native_partition(start: int, count: int, rank: int, world: int) -> tuple[int, int]:
+    """pow_group_partition of the C ABI (must equal :func:`partition`)."""
+    s, n = ctypes.c_uint64(), ctypes.c_uint64()
+    load().pow_group_partition(start, count, rank, world, ctypes.byref(s), ctypes.byref(n))
+    return s.value, n.value
 
 
-def sharded_mine(search: Callable[[int, int], Optional[int]],
-                 allreduce_min: Callable[[int], int],
-                 start: int, count: int, round_size: int, rank: int, world: int,
-                 difficulty: int = 0) -> Optional[int]:
-    """Lowest solving counter of [start, start+count) over all ranks.
+class _Group:
+    """A ``pow_group``: the collective sharded search of include/pow_gpu.h."""
 
-    search(s, n)        -> lowest solving counter in [s, s+n) on this rank, or None
-    allreduce_min(v)    -> min of v over ranks (v = NONE when nothing found)
-    round_size 0        -> adaptive rounds for `difficulty` (round_plan)
-    Every rank returns the same value.
-    """
-    adaptive = round_size == 0
-    if adaptive:
-        round_size, big = round_plan(world, difficulty)
-    done = 0
-    while done < count:
-        n = min(round_size, count - done)
-        s, k = partition(start + done, n, rank, world)
-        local = search(s, k) if k > 0 else None
-        best = allreduce_min(NONE if local is None else local)
-        if best != NONE:
-            return best
-        done += n
-        if adaptive:
-            round_size = min(big, round_size * 4)
-    return None
+    miner = None
+    g = ctypes.c_void_p()
+
+    def allreduce(self, vals, op: str = "min") -> list[int]:
+        """In-place all-reduce of <= 8 uint64 over the group's ranks."""
+        arr = (ctypes.c_uint64 * len(vals))(*vals)
+        code = {"min": POW_REDUCE_MIN, "max": POW_REDUCE_MAX, "sum": POW_REDUCE_SUM}[op]
+        check(load().pow_group_allreduce_u64(self.g, arr, len(vals), code))
+        return list(arr)
+
+    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
+             epoch: int | None = None, any_solution: bool = False):
+        """Lowest solving counter of [start, start+count) over all ranks
+        (pow_group_mine), or with ``any_solution`` the first solution any GPU
+        finds (pow_group_mine_any: the finder stops the node's other GPUs
+        through the stop board).  Collective.  The same MineResult on every
+        rank, or None (no solution / cancelled on some rank); raises PowError
+        on every rank if any rank failed.  ``hashes`` and ``kernel_ms`` are
+        this rank's, summed over the rounds."""
+        from .miner import MineResult
+
+        out = Block()
+        ctr, hashes = ctypes.c_uint64(), ctypes.c_uint64()
+        m = self.miner
+        ep = m.epoch if epoch is None else epoch
+        fn = m.L.pow_group_mine_any if any_solution else m.L.pow_group_mine
+        rc = check(fn(self.g, ctypes.byref(tmpl), start, count, round_size, difficulty,
+                      ctypes.byref(m._cancel), ep, ctypes.byref(out), ctypes.byref(ctr),
+                      ctypes.byref(hashes)))
+        if rc == 0:
+            return None
+        return MineResult(out, ctr.value, hashes.value, m.stats()["kernel_ms"])
+
+    def close(self) -> None:
+        if self.g:
+            load().pow_group_destroy(self.g)
+            self.g = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
-def torch_allreduce_min(device=None, group=None) -> Callable[[int], int]:
-    """8-byte all-reduce(MIN) through torch.distributed (RCCL when the
-    process group is nccl and `device` is a GPU; gloo on CPU for tests)."""
-    import torch
-    import torch.distributed as dist
-
-    buf = torch.zeros(1, dtype=torch.int64, device=device or "cpu")
-
-    def f(v: int) -> int:
-        buf.fill_(v)
-        dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
-        return int(buf.item())
-
-    return f
-
-
-class RcclGroup:
-    """The same sharded search done natively: ``pow_group_*`` of
-    libpow_gpu.so (mpi_blockchain_amd/csrc/pow_group.cpp) runs the rounds in
-    C++ and calls RCCL itself (one 24-byte ``ncclAllReduce(ncclMin)`` per
-    round for winner, cancellation and failure).  This is the form a C/C++
-    caller — the reference's node is C++ — uses; ranks exchange the 128-byte
-    RCCL id by any means (``from_torch`` uses torch.distributed)."""
+class RcclGroup(_Group):
+    """``pow_group_init``: the sharded search over RCCL (one 24-byte
+    ``ncclAllReduce(ncclMin)`` per round, called from C++).  This is the form
+    a C/C++ caller — the reference's node is C++ — uses; ranks exchange the
+    128-byte RCCL id by any means (``from_torch`` uses torch.distributed)."""
 
     def __init__(self, miner, rank: int, world: int, unique_id: bytes):
-        from ._lib import GROUP_ID_BYTES, check
+        from ._lib import GROUP_ID_BYTES
 
         if len(unique_id) != GROUP_ID_BYTES:
             raise ValueError("unique_id must be 128 bytes")
@@ -99,7 +115,7 @@ class RcclGroup:
 
     @staticmethod
     def make_unique_id() -> bytes:
-        from ._lib import GROUP_ID_BYTES, check, load
+        from ._lib import GROUP_ID_BYTES
 
         buf = ctypes.create_string_buffer(GROUP_ID_BYTES)
         check(load().pow_group_unique_id(buf))
@@ -124,103 +140,61 @@ class RcclGroup:
             raise RuntimeError(obj[0])
         return cls(miner, dist.get_rank(group), dist.get_world_size(group), obj[0])
 
-    def allreduce(self, vals, op: str = "min") -> list[int]:
-        from ._lib import POW_REDUCE_MAX, POW_REDUCE_MIN, POW_REDUCE_SUM, check
 
-        arr = (ctypes.c_uint64 * len(vals))(*vals)
-        code = {"min": POW_REDUCE_MIN, "max": POW_REDUCE_MAX, "sum": POW_REDUCE_SUM}[op]
-        check(self.miner.L.pow_group_allreduce_u64(self.g, arr, len(vals), code))
-        return list(arr)
+def torch_reduction(device=None, group=None):
+    """f(vals, op) -> vals all-reduced over a torch.distributed group
+    (op = POW_REDUCE_*).  uint64 words travel as int64: MIN/MAX shifted by
+    2^63 (order-preserving), SUM as two's complement (mod 2^64)."""
+    import torch
+    import torch.distributed as dist
 
-    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
-             epoch: int | None = None, any_solution: bool = False):
-        """Lowest solving counter of [start, start+count) over all ranks
-        (pow_group_mine), or with ``any_solution`` the first solution any GPU
-        finds (pow_group_mine_any: the finder stops the node's other GPUs
-        through the stop board).  The same MineResult on every rank;
-        ``hashes`` and ``kernel_ms`` are this rank's, summed over the rounds."""
-        from ._lib import Block, check
-        from .miner import MineResult
+    ops = {POW_REDUCE_MIN: dist.ReduceOp.MIN, POW_REDUCE_MAX: dist.ReduceOp.MAX,
+           POW_REDUCE_SUM: dist.ReduceOp.SUM}
 
-        out = Block()
-        ctr, hashes = ctypes.c_uint64(), ctypes.c_uint64()
-        m = self.miner
-        ep = m.epoch if epoch is None else epoch
-        fn = m.L.pow_group_mine_any if any_solution else m.L.pow_group_mine
-        rc = check(fn(self.g, ctypes.byref(tmpl), start, count, round_size, difficulty,
-                      ctypes.byref(m._cancel), ep, ctypes.byref(out), ctypes.byref(ctr),
-                      ctypes.byref(hashes)))
-        if rc == 0:
-            return None
-        return MineResult(out, ctr.value, hashes.value, m.stats()["kernel_ms"])
+    def f(vals: list[int], op: int) -> list[int]:
+        if op == POW_REDUCE_SUM:
+            enc = [v - _U64 if v >= _HALF else v for v in vals]
+        else:
+            enc = [v - _HALF for v in vals]
+        t = torch.tensor(enc, dtype=torch.int64, device=device or "cpu")
+        dist.all_reduce(t, op=ops[op], group=group)
+        out = t.tolist()
+        return [v % _U64 for v in out] if op == POW_REDUCE_SUM else [v + _HALF for v in out]
 
-    def close(self) -> None:
-        if self.g:
-            self.miner.L.pow_group_destroy(self.g)
-            self.g = ctypes.c_void_p()
-
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *exc):
-        self.close()
+    return f
 
 
-def native_partition(start: int, count: int, rank: int, world: int) -> tuple[int, int]:
-    """pow_group_partition of the C ABI (must equal :func:`partition`)."""
-    from ._lib import load
+class ShardedMiner(_Group):
+    """The sharded search (C++ rounds of pow_group_*) for one rank, with its
+    all-reduce done by torch.distributed (``pow_group_init_custom``): gloo on
+    CPU, or the ranks of a test that share one GPU.  With ``board`` (default)
+    the ranks of one node share a stop board, its name made by rank 0 and
+    broadcast.  ``miner=None`` builds a group that only carries
+    :meth:`allreduce` (no GPU needed)."""
 
-    s, n = ctypes.c_uint64(), ctypes.c_uint64()
-    load().pow_group_partition(start, count, rank, world, ctypes.byref(s), ctypes.byref(n))
-    return s.value, n.value
+    def __init__(self, miner, rank: int, world: int, device=None, group=None, board: bool = True):
+        import torch.distributed as dist
 
-
-class ShardedMiner:
-    """GPU-backed sharded search for one rank (one GPU per process) over
-    torch.distributed.  With ``board=True`` the ranks of one node also share a
-    stop board (its name broadcast from rank 0), so a rank's hit stops the
-    others inside their running launches, as pow_group_* do natively."""
-
-    def __init__(self, miner, rank: int, world: int, device=None, group=None, board: bool = False):
         self.miner, self.rank, self.world = miner, rank, world
-        self.allreduce_min = torch_allreduce_min(device, group)
-        self.board, self._searches = None, 0
-        if board and world <= 64:
-            import os
-            import uuid
+        self.g = ctypes.c_void_p()
+        self.reduce_error: Exception | None = None
+        red = torch_reduction(device, group)
 
-            import torch.distributed as dist
+        def cb(_user, vals, n, op):
+            try:
+                out = red([vals[i] for i in range(n)], op)
+                for i, v in enumerate(out):
+                    vals[i] = v
+                return 0
+            except Exception as e:  # reported through the C call's POW_ECOMM
+                self.reduce_error = e
+                return 1
 
-            from .miner import StopBoard
-
-            obj = [f"/pow_board_{os.getpid()}_{uuid.uuid4().hex[:12]}" if rank == 0 else None]
+        self._cb = REDUCE_FN(cb)  # kept alive as long as the group
+        name = None
+        if board and miner is not None and world <= 64:
+            obj = [f"/pow_board_{os.getpid()}_{uuid.uuid4().hex[:12]}" if dist.get_rank(group) == 0 else None]
             dist.broadcast_object_list(obj, src=0, group=group)
-            self.board = StopBoard(world, obj[0])
-            dist.barrier(group=group)  # every rank has it mapped: the name can go
-            self.board.unlink()
-
-    def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
-             any_solution: bool = False):
-        """Lowest solving counter over all ranks, or (``any_solution``) the
-        lowest of the counters the ranks found first in the winning round."""
-        if self.board is not None:
-            self._searches += 1
-            self.miner.bind_board(self.board, self.rank, 1 + (self._searches - 1) % 1023)
-
-        def search(s, n):
-            r = self.miner.mine(tmpl, s, n, difficulty, any_solution=any_solution)
-            return None if r is None else r.counter
-
-        try:
-            return sharded_mine(search, self.allreduce_min, start, count,
-                                (self.world << 32 if any_solution and not round_size else round_size),
-                                self.rank, self.world, difficulty)
-        finally:
-            if self.board is not None:
-                self.miner.bind_board(None)
-
-    def close(self) -> None:
-        if self.board is not None:
-            self.miner.bind_board(None)
-            self.board.close()
-            self.board = None
+            name = obj[0]
+        check(load().pow_group_init_custom(miner.ctx if miner is not None else None, world, rank, self._cb, None,
+                                           name.encode() if name else None, ctypes.byref(self.g)))

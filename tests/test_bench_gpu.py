@@ -29,11 +29,40 @@ def test_bench_json_contract():
     assert r["bound"] and r["peak"] > 0 and 0 < r["frac"] < 1.5
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert d["parity"]["count_ok"] is True
+    # the timed step's own output: its sorted list's sha256 equals the golden fingerprint
+    assert d["parity"]["fingerprint_ok"] is True, d["parity"]
     # traffic measured in the run (two rocprofv3 PMC passes): at least the
     # solution list (4 B per solution), at most a few times it
-    assert "total_bytes" in r["traffic_live"], r["traffic_live"]
-    assert r["traffic"] == r["traffic_live"]["total_bytes"] and "measured in this run" in r["traffic_source"]
+    live = r["counters_live"]
+    assert "total_bytes" in live, live
+    assert r["traffic"] == live["total_bytes"] and "measured in this run" in r["traffic_source"]
     assert r["algorithmic_bytes"] <= r["traffic"] < 4 * r["algorithmic_bytes"], r
+    # the VALU counter pass: ~4,837 VALU instructions per hash, a clock near 2.4 GHz
+    assert 4700 < r["valu_instr_per_hash"] < 5000, live
+    assert 1.5 < r["measured_clock_ghz"] < 2.5 and 2.0 <= r["cycles_per_valu_instr"] < 6, live
+    assert 0 < r["issued_frac_at_measured_clock"] <= r["frac_at_measured_clock"] < 1.0, r
+
+
+def test_valu_microbench_ceilings():
+    """pow_valu_rate: the full-rate chain issues faster than the half-rate one
+    (about 2x), each at a measured clock; the mix-adjusted ceiling lies
+    between them."""
+    import ctypes
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from mpi_blockchain_amd._lib import POW_VALU_FULL, POW_VALU_HALF, POW_VALU_MIX, ValuResult, load
+
+    L = load()
+    out = {}
+    for k in (POW_VALU_FULL, POW_VALU_HALF, POW_VALU_MIX):
+        r = ValuResult()
+        assert L.pow_valu_rate(0, k, ctypes.byref(r)) == 0
+        assert 1.0e9 < r.clock_hz < 2.6e9 and r.lane_ops_per_s > 1e12, (k, r.clock_hz, r.lane_ops_per_s)
+        out[k] = r
+    assert 1.5 < out[POW_VALU_FULL].lane_ops_per_s / out[POW_VALU_HALF].lane_ops_per_s < 2.5
+    assert 1.9 < out[POW_VALU_FULL].cycles_per_instr < 2.6 and 3.6 < out[POW_VALU_HALF].cycles_per_instr < 4.6
+    assert L.pow_valu_rate(0, 7, ctypes.byref(ValuResult())) < 0
 
 
 def run_rehearsal(n: int) -> dict:
@@ -56,7 +85,10 @@ def run_rehearsal(n: int) -> dict:
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 1e9
-    assert "gloo all_reduce" in d["config"]["parallelism"]
+    assert "gloo all_reduce" in d["config"]["parallelism"] and "pow_group_init_custom" in d["config"]["parallelism"]
+    # config 4's cooperative search ran through pow_group's C++ rounds on every rank
+    gs = d["group_search"]
+    assert gs["n_gpus"] == n and gs["templates"] == 21 and gs["hashes_all_ranks_mean"] > 0, gs
     assert "cpu_baseline" not in d and "ladder" not in d  # rank-0-at-N=1-only extras
     # config 5 at the job's size: mpiexec -np n pow_node (here all on the one GPU)
     pr = d["protocol"]

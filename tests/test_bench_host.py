@@ -1,6 +1,8 @@
-"""Host logic of bench.py that needs no GPU: the live PMC traffic passes
-(pmc_traffic_live) parse rocprofv3's counter CSV, drop pow_warmup's empty
-dispatch, take the median per sweep dispatch and convert KiB to bytes."""
+"""Host logic of bench.py that needs no GPU: the live PMC passes (pmc_live)
+parse rocprofv3's counter and kernel-trace CSVs, drop pow_warmup's empty
+dispatch, take the median per sweep dispatch, convert KiB to bytes, and derive
+VALU instructions per hash, the clock and cycles per instruction; the
+roofline block and the CPU-baseline headline."""
 import csv
 import os
 import shutil
@@ -15,22 +17,41 @@ import bench  # noqa: E402
 K1 = "void pow_search<0, false>(PowConsts const*, PowLaunch, unsigned int*, PowResult*)"
 
 
+DUR_NS = [1_000, 496_500_000, 496_300_000, 497_000_000]  # first: pow_warmup's launch
+VALU = {"SQ_INSTS_VALU": [10.0, 324614173324.0, 324614173640.0, 324614172846.0],
+        "SQ_ACTIVE_INST_VALU": [10.0, 324614189694.0, 324614190008.0, 324614189216.0],
+        "GRBM_GUI_ACTIVE": [100.0, 9472254275.0, 9473312216.0, 9474333110.0]}
+
+
 def fake_run(values_kib, rc=0, grid=True):
-    """A stand-in for subprocess.run that writes what `rocprofv3 --pmc C -d DIR`
-    would: one row per (dispatch, counter) in DIR/<host>/<pid>_counter_collection.csv.
-    The first dispatch is pow_warmup's one-workgroup launch."""
+    """A stand-in for subprocess.run that writes what `rocprofv3 --pmc C.. -d DIR
+    [--kernel-trace]` would: one row per (dispatch, counter) in
+    DIR/<host>/<pid>_counter_collection.csv (and the kernel trace).  The first
+    dispatch is pow_warmup's one-workgroup launch."""
 
     def run(cmd, cwd=None, **kw):
-        counter = cmd[cmd.index("--pmc") + 1]
+        i = cmd.index("--pmc") + 1
+        counters = []
+        while not cmd[i].startswith("-"):
+            counters.append(cmd[i])
+            i += 1
         out = os.path.join(cmd[cmd.index("-d") + 1], "host")
         os.makedirs(out, exist_ok=True)
+        vals = dict(values_kib, **VALU)
         with open(os.path.join(out, "1_counter_collection.csv"), "w", newline="") as f:
             w = csv.writer(f)
             w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"] + (["Grid_Size"] if grid else []))
-            for i, v in enumerate(values_kib[counter]):
-                w.writerow([i + 1, K1, counter, v] + ([256 if i == 0 else 524032] if grid else []))
-            w.writerow([99, "void pow_hash_kernel(unsigned int const*, unsigned int, unsigned int*)", counter, 1e6]
-                       + ([64] if grid else []))
+            for counter in counters:
+                for i, v in enumerate(vals[counter]):
+                    w.writerow([i + 1, K1, counter, v] + ([256 if i == 0 else 524032] if grid else []))
+                w.writerow([99, "void pow_hash_kernel(unsigned int const*, unsigned int, unsigned int*)", counter,
+                            1e6] + ([64] if grid else []))
+        if "--kernel-trace" in cmd:
+            with open(os.path.join(out, "1_kernel_trace.csv"), "w", newline="") as f:
+                w = csv.writer(f)
+                w.writerow(["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+                for i, dns in enumerate(DUR_NS):
+                    w.writerow([i + 1, K1, 1000, 1000 + dns])
         return subprocess.CompletedProcess(cmd, rc, "", "")
 
     return run
@@ -42,7 +63,7 @@ def test_live_traffic_median_without_warmup(monkeypatch):
     vals = {"FETCH_SIZE": [5.0625, 734.125, 746.8125, 734.0],      # first: pow_warmup's empty launch
             "WRITE_SIZE": [0.125, 71545.90625, 71559.75, 71548.0625]}
     monkeypatch.setattr(bench.subprocess, "run", fake_run(vals))
-    r = bench.pmc_traffic_live()
+    r = bench.pmc_live(256)
     assert r["FETCH_SIZE"]["kib_per_dispatch"] == [734.0, 734.125, 746.8125]
     assert r["FETCH_SIZE"]["median_bytes"] == int(734.125 * 1024)
     assert r["WRITE_SIZE"]["median_bytes"] == int(71548.0625 * 1024)
@@ -59,7 +80,7 @@ def test_live_traffic_robust_to_an_outlier_dispatch(monkeypatch):
             "WRITE_SIZE": [0.125, 71545.90625, 71559.75, 71548.0625]}
     for grid in (True, False):
         monkeypatch.setattr(bench.subprocess, "run", fake_run(vals, grid=grid))
-        r = bench.pmc_traffic_live()
+        r = bench.pmc_live(256)
         assert r["FETCH_SIZE"]["kib_per_dispatch"] == [734.125, 746.8125, 80000.0], (grid, r)
         assert r["FETCH_SIZE"]["median_bytes"] == int(746.8125 * 1024)
 
@@ -69,12 +90,68 @@ def test_live_traffic_reports_a_failed_pass(monkeypatch):
     monkeypatch.setattr(bench.os, "access", lambda p, m: True)
     vals = {"FETCH_SIZE": [734.0], "WRITE_SIZE": [71548.0]}  # too few sweep dispatches
     monkeypatch.setattr(bench.subprocess, "run", fake_run(vals, rc=0))
-    r = bench.pmc_traffic_live()
+    r = bench.pmc_live(256)
     assert "error" in r and "total_bytes" not in r
     monkeypatch.setattr(bench.subprocess, "run", fake_run({"FETCH_SIZE": [1.0] * 3, "WRITE_SIZE": [1.0] * 3}, rc=137))
-    assert "error" in bench.pmc_traffic_live()
+    assert "error" in bench.pmc_live(256)
 
 
 def test_live_traffic_without_profiler(monkeypatch):
     monkeypatch.setattr(shutil, "which", lambda name: None)
-    assert "error" in bench.pmc_traffic_live()
+    assert "error" in bench.pmc_live(256)
+
+
+def test_live_valu_counters(monkeypatch):
+    """The third pass: VALU wave-instructions x 64 / 2^32 per hash (r02: 4,837),
+    the clock from GRBM_GUI_ACTIVE (summed over 8 XCDs) over the same
+    dispatch's duration, cycles per VALU instruction per SIMD."""
+    monkeypatch.setattr(shutil, "which", lambda name: "/usr/bin/rocprofv3")
+    monkeypatch.setattr(bench.os, "access", lambda p, m: True)
+    vals = {"FETCH_SIZE": [5.0, 734.0, 735.0, 736.0], "WRITE_SIZE": [0.1, 71545.0, 71546.0, 71547.0]}
+    monkeypatch.setattr(bench.subprocess, "run", fake_run(vals))
+    v = bench.pmc_live(256)["valu"]
+    assert v["dispatches"] == 3 and v["kernel_ns"] == 496_500_000  # the median duration
+    assert abs(v["valu_instr_per_hash"] - 4837.1) < 0.1
+    clk = 9472254275.0 / 8 / 0.4965
+    assert abs(v["clock_ghz"] - clk / 1e9) < 1e-4
+    assert abs(v["cycles_per_valu_instr"] - 1024 * clk * 0.4965 / 324614173324.0) < 1e-3
+    r = bench.roofline_block(43.28, 496.2, {"nominal_tops": 78.64}, {"valu": v}, 1, "x", 1, 256)
+    assert r["valu_instr_per_hash"] == v["valu_instr_per_hash"]
+    assert abs(r["frac_at_measured_clock"] - 43.28 / (1024 * 32 * clk / 1e12)) < 1e-4
+    assert 0 < r["issued_frac_at_measured_clock"] < r["frac_at_measured_clock"]
+
+
+def test_mix_adjusted_ceiling_math():
+    """The ceiling prices K1's trial mix at the isolated full- and half-rate
+    microbenchmark rates: with the r01 probe's 2.2 / 4.1 cycles at 2.38 GHz it
+    is ~9.8 G hashes/s."""
+    f_tops = 1024 * 64 * 2.38e9 / 2.2 / 1e12
+    h_tops = 1024 * 64 * 2.38e9 / 4.1 / 1e12
+    hps = 1.0 / (bench.TRIAL_HALF_RATE / (h_tops * 1e12) + bench.TRIAL_FULL_RATE / (f_tops * 1e12))
+    assert 9.7e9 < hps < 9.9e9
+    assert bench.TRIAL_HALF_RATE + bench.TRIAL_FULL_RATE == 4831
+
+
+def test_cpu_baseline_headline_is_the_best_run(monkeypatch):
+    """cpu_baseline's value is the best reference rate among the runs (at the
+    cgroup quota on the GPU box) and `cores` the CPUs the job can use."""
+    import json as _json
+
+    monkeypatch.setattr(bench, "host_cpu_info", lambda: {"affinity": 256, "cgroup_cpu_quota": 16.0,
+                                                        "sockets": "2", "cores_per_socket": "64"})
+    rates = {("O2", 256): 3.4e6, ("O0", 256): 5.3e5, ("O2", 16): 4.99e6}
+
+    def run(cmd, **kw):
+        flav = os.path.basename(cmd[-2])[-2:] if "mpiexec" in cmd[4] else os.path.basename(cmd[0])[-2:]
+        np_ = int(cmd[cmd.index("-np") + 1])
+        return subprocess.CompletedProcess(cmd, 0, _json.dumps({"ranks": np_, "trials_per_s": rates[(flav, np_)]}), "")
+
+    monkeypatch.setattr(bench.subprocess, "run", run)
+    monkeypatch.setattr(bench.os.path, "exists", lambda p: True)
+    import mpi_blockchain_amd.build as B
+    monkeypatch.setattr(B, "mpi_available", lambda: True)
+    r = bench.cpu_baseline()
+    assert r["value"] == 4.99e6 and r["cores"] == 16 and r["headline_run"] == "O2_at_quota"
+    assert r["value"] >= r["at_cpu_quota"]["value"]
+    assert r["logical_cpus"] == 256 and r["physical_cores"] == 128 and r["usable_cpus"] == 16.0
+    assert r["as_shipped_O0"] == 5.3e5

@@ -119,3 +119,44 @@ def test_latency_kernel_no_private_copy(isa, variant):
     assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 64
     # one trial per lane, nothing hoisted across j: 5,083 VALU (K1: 4,831)
     assert 5000 <= len(re.findall(r"^\s+v_", body, flags=re.M)) <= 5120
+
+
+def test_trial_issue_mix_matches_bench(isa):
+    """bench.py's mix-adjusted ceiling prices K1's trial by its issue classes
+    (TRIAL_HALF_RATE / TRIAL_FULL_RATE); they must be the ISA's: half rate =
+    v_alignbit_b32, v_add3_u32 and any other op with an SGPR operand."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    body = j_loop_body(isa, "_Z10pow_searchILi0ELb0E")
+    lines = [ln.strip() for ln in body.splitlines() if re.match(r"\s+v_", ln)]
+    half = [ln for ln in lines if ln.split()[0] in ("v_alignbit_b32", "v_add3_u32")
+            or re.search(r"\bs\d+\b|\bs\[", ln)]
+    assert (len(half), len(lines) - len(half)) == (bench.TRIAL_HALF_RATE, bench.TRIAL_FULL_RATE)
+
+
+def test_valu_microbench_streams():
+    """pow_valu_rate's three loops issue exactly the instruction kinds they are
+    named for (the full-rate one must not fuse into half-rate v_xad_u32), with
+    VGPR operands only."""
+    import collections
+
+    from mpi_blockchain_amd.build import hipcc
+
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-mcode-object-version=5",
+                        "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c",
+                        os.path.join(CSRC, "valu_peak.hip"), "-o", os.path.join(td, "v.o"),
+                        "-save-temps=obj"], check=True, cwd=td, capture_output=True)
+        s = open(os.path.join(td, [f for f in os.listdir(td) if f.endswith("gfx950.s")][0])).read()
+    want = {"ILi0E": {"v_alignbit_b32", "v_bitop3_b32", "v_add3_u32"},
+            "ILi1E": {"v_bitop3_b32", "v_add_u32_e32"},
+            "ILi2E": {"v_alignbit_b32", "v_add3_u32"}}
+    for k, kinds in want.items():
+        body = j_loop_body(s, "_Z16valu_rate_kernel" + k)
+        ops = [ln.strip() for ln in body.splitlines() if re.match(r"\s+v_", ln)]
+        c = collections.Counter(o.split()[0] for o in ops)
+        assert set(c) == kinds and len(set(c.values())) == 1, (k, c)  # equal counts: one of each per step
+        assert not [o for o in ops if re.search(r"\bs\d+\b|\bs\[", o)], k

@@ -1,15 +1,17 @@
-"""Sharded search logic (mpi_blockchain_amd/shard.py), CPU only: static
-partition, min-counter winner, and a real world_size-2 run over
-torch.distributed gloo (the same all-reduce(MIN) code path the GPU ranks use
-over RCCL).  The per-rank search is the CPU oracle here — this tests the
-sharding and the collective, not the kernel."""
+"""Sharded search (pow_group_*, mpi_blockchain_amd/shard.py), CPU only.
+
+The search rounds themselves run in C++ (csrc/pow_group.cpp) and need a GPU:
+tests/test_shard_gpu.py drives them with 1, 2 and 4 ranks.  Here: the static
+partition (Python mirror == C ABI), and the custom-reduction group
+(pow_group_init_custom over torch.distributed gloo) at world size 2 and 4 in
+real processes: its joining barrier, the uint64 encoding of min/max/sum, and
+the checks a group without a GPU context makes."""
 import os
 import socket
 
 import pytest
 
-from mpi_blockchain_amd.shard import NONE, partition, sharded_mine
-from oracle.oracle import Oracle, make_oblock
+from mpi_blockchain_amd.shard import partition
 
 
 def test_partition_covers_range():
@@ -22,46 +24,6 @@ def test_partition_covers_range():
             assert sum(n for _, n in parts) == count
 
 
-def _simulated_world(search, start, count, round_size, world):
-    """Run every rank's search per round and reduce by hand (what RCCL does)."""
-    done = 0
-    while done < count:
-        n = min(round_size, count - done)
-        best = NONE
-        for r in range(world):
-            s, k = partition(start + done, n, r, world)
-            v = search(s, k) if k else None
-            best = min(best, NONE if v is None else v)
-        if best != NONE:
-            return best
-        done += n
-    return None
-
-
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_sharded_equals_single(world):
-    O = Oracle()
-    b = make_oblock(1, 0, 9, 1700000000, b"")
-
-    def search(s, n):
-        return O.mine(b, s, n, 13)
-
-    single = O.mine(b, 0, 1 << 15, 13)
-    # the first solution at d = 13 is 6399 (SURVEY §8c)
-    assert single == 6399
-    for rs in (1000, 4096, 1 << 15):
-        assert _simulated_world(search, 0, 1 << 15, rs, world) == single
-    # rank-local view through sharded_mine with a fake reduction
-    calls = []
-
-    def fake_min(v):
-        calls.append(v)
-        return v
-
-    got = sharded_mine(search, fake_min, 6000, 1000, 1000, 0, 1)
-    assert got == 6399 and calls == [6399]
-
-
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -70,43 +32,93 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+U64MAX = (1 << 64) - 1
+
+
+def _custom_group_worker(rank, world, port, q):
+    import ctypes
+
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mpi_blockchain_amd.shard import torch_allreduce_min
+    from mpi_blockchain_amd import _lib
+    from mpi_blockchain_amd.shard import ShardedMiner
 
-    O = Oracle()
-    b = make_oblock(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
-    red = torch_allreduce_min()
-    res = []
-    for start, count, rs, d in ((0, 1 << 12, 1 << 12, 9), (300, 5000, 2048, 9), (0, 40000, 8192, 13),
-                                (0, 40000, 0, 13)):  # rs 0: adaptive rounds (round_plan)
-        res.append(sharded_mine(lambda s, n: O.mine(b, s, n, d), red, start, count, rs, rank, world, d))
-    q.put((rank, res))
+    out = {}
+    with ShardedMiner(None, rank, world) as g:  # no GPU context: collectives only
+        # the extremes of the uint64 range survive the int64 transport
+        vals = [rank, U64MAX - rank, (1 << 63) + rank, 7 if rank == world - 1 else U64MAX]
+        out["min"] = g.allreduce(vals, "min")
+        out["max"] = g.allreduce(vals, "max")
+        out["sum"] = g.allreduce([rank + 1, (1 << 63) + rank, U64MAX], "sum")
+        # the round consensus word {counter, go, ok}: one rank cancelled
+        out["consensus"] = g.allreduce([U64MAX if rank else 12345, 0 if rank == world - 1 else 1, 1], "min")
+        blk = _lib.Block()
+        out["mine_rc"] = _lib.load().pow_group_mine(g.g, ctypes.byref(blk), 0, 1, 0, 9, None, 0, ctypes.byref(blk),
+                                                    None, None)
+    q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_world2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_custom_group_collectives(world):
+    """pow_group_init_custom over gloo in `world` processes: every rank joins
+    (the init barrier checks the rank count), min/max/sum are exact over the
+    whole uint64 range, and a group without a context refuses to mine."""
     import torch.multiprocessing as mp
+
+    from mpi_blockchain_amd import _lib
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_custom_group_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    O = Oracle()
-    b = make_oblock(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
-    want = [O.mine(b, 0, 1 << 12, 9), O.mine(b, 300, 5000, 9), O.mine(b, 0, 40000, 13), O.mine(b, 0, 40000, 13)]
-    assert want[0] == 263  # golden: first S1 solution
-    assert out[0] == out[1] == want
+    try:
+        out = dict(q.get(timeout=120) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    want_min = [0, U64MAX - (world - 1), 1 << 63, 7]
+    want_max = [world - 1, U64MAX, (1 << 63) + world - 1, U64MAX]
+    want_sum = [world * (world + 1) // 2, ((1 << 63) * world + world * (world - 1) // 2) % (1 << 64),
+                (U64MAX * world) % (1 << 64)]
+    for r in range(world):
+        assert out[r]["min"] == want_min
+        assert out[r]["max"] == want_max
+        assert out[r]["sum"] == want_sum
+        assert out[r]["consensus"] == [12345, 0, 1]
+        assert out[r]["mine_rc"] == _lib.POW_EINVAL
+
+
+def test_custom_group_rank_count_mismatch():
+    """A group whose ranks disagree on its size fails to form: the joining
+    barrier counts the ranks that called it (one process, world 1, told 2)."""
+    import ctypes
+
+    from mpi_blockchain_amd import _lib
+
+    L = _lib.load()
+    calls = []
+
+    def red(_u, vals, n, op):
+        calls.append((n, op, vals[0]))
+        return 0  # a "reduction" over the one rank that is really there
+
+    fn = _lib.REDUCE_FN(red)
+    g = ctypes.c_void_p()
+    assert L.pow_group_init_custom(None, 2, 0, fn, None, None, ctypes.byref(g)) == _lib.POW_ECOMM and not g
+    assert calls == [(1, _lib.POW_REDUCE_SUM, 1)]
+    assert b"1 ranks joined a group of 2" in L.pow_last_error()
+    # a failing reduction is POW_ECOMM; a null reduction or a bad rank is POW_EINVAL
+    fail = _lib.REDUCE_FN(lambda *a: 1)
+    assert L.pow_group_init_custom(None, 1, 0, fail, None, None, ctypes.byref(g)) == _lib.POW_ECOMM and not g
+    assert L.pow_group_init_custom(None, 1, 0, _lib.REDUCE_FN(), None, None, ctypes.byref(g)) == _lib.POW_EINVAL
+    assert L.pow_group_init_custom(None, 1, 1, fn, None, None, ctypes.byref(g)) == _lib.POW_EINVAL
 
 
 def test_native_partition_matches():
@@ -137,27 +149,6 @@ def test_group_unique_id_and_arg_checks():
     assert L.pow_group_mine(None, ctypes.byref(blk), 0, 1, 0, 9, None, 0, ctypes.byref(blk), None, None) \
         == _lib.POW_EINVAL
     assert L.pow_group_allreduce_u64(None, None, 0, 0) == _lib.POW_EINVAL
-
-
-def test_round_plan_adaptive():
-    """Adaptive rounds (round_size 0): first round ~4x the expected trials,
-    at least 2^16 per rank, growing 4x up to 2^30 per rank; the winner equals
-    one search over the whole range (multi-rank: test_gloo_world2)."""
-    from mpi_blockchain_amd.shard import round_plan
-
-    assert round_plan(8, 25) == (1 << 27, 8 << 30)
-    assert round_plan(2, 9) == (2 << 16, 2 << 30)
-    assert round_plan(1, 60)[0] == 1 << 30
-    O = Oracle()
-    b = make_oblock(1, 0, 9, 1700000000, b"")
-    for d in (9, 13, 17):
-        sizes = []
-
-        def search(s, n):
-            sizes.append(n)
-            return O.mine(b, s, n, d)
-        assert sharded_mine(search, lambda v: v, 0, 1 << 20, 0, 0, 1, d) == O.mine(b, 0, 1 << 20, d)
-        assert sizes[0] == round_plan(1, d)[0] and all(y == 4 * x for x, y in zip(sizes, sizes[1:-1]))
 
 
 def test_board_host_protocol():

@@ -1,6 +1,15 @@
-"""ShardedMiner on the GPU: pow_mine per shard + the torch.distributed
-all-reduce(min) (gloo here, world size 1; RCCL in bench.py) returns the same
-counter as one un-sharded pow_mine."""
+"""The sharded search pow_group_* on the GPU (BASELINE config 4).
+
+The C++ rounds, the stop board and the {counter, go, ok} consensus of
+csrc/pow_group.cpp run here with 1, 2 and 4 ranks.  RCCL refuses two ranks on
+one device and this pool gives one GPU per call, so the multi-rank tests
+build the group with pow_group_init_custom over torch.distributed gloo
+(ShardedMiner): every rank is its own process with its own pow_ctx on the one
+GPU, and only the one all-reduce per round changes transport.  RCCL itself
+(pow_group_init) runs at world size 1 below; the 8-GPU run is the driver's.
+
+Expected values are golden (tests/golden/fingerprints_2p32.json):
+S0's first solutions at d = 13, 21, 25 are 6399, 2392323 and 73523910."""
 import os
 import socket
 
@@ -10,39 +19,156 @@ from mpi_blockchain_amd.block import make_block
 
 pytestmark = pytest.mark.gpu
 
+S1_PREV = b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8"
 
-def test_sharded_equals_unsharded():
-    import torch.distributed as dist
 
-    from mpi_blockchain_amd.miner import GpuMiner
-    from mpi_blockchain_amd.shard import ShardedMiner, sharded_mine
-
+def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return port
+
+
+def test_sharded_world1_equals_unsharded():
+    """One rank: pow_group_mine over the custom (gloo) reduction returns
+    exactly pow_mine's lowest counter, nonce and hash, for adaptive rounds,
+    small unaligned rounds and one big round."""
+    import torch.distributed as dist
+
+    from mpi_blockchain_amd.miner import GpuMiner
+    from mpi_blockchain_amd.shard import ShardedMiner
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        with GpuMiner(0) as m:
-            b = make_block(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
-            sm = ShardedMiner(m, 0, 1)
-            for d in (9, 13, 17):
-                want = m.mine(b, 0, 1 << 24, d)
-                got = sm.mine(b, 0, 1 << 24, d, round_size=1 << 20)
-                assert want is not None and got == want.counter
-            # 3 simulated ranks over the same range, each mining its shard on the GPU
-            def search(start, n):
-                r = m.mine(b, start, n, 13)
-                return None if r is None else r.counter
-            from mpi_blockchain_amd.shard import NONE, partition
-            best = NONE
-            for rank in range(3):
-                v = sharded_mine(search, lambda x: x, 0, 1 << 20, 1 << 20, rank, 3)
-                best = min(best, NONE if v is None else v)
-            assert best == m.mine(b, 0, 1 << 20, 13).counter
+        with GpuMiner(0) as m, ShardedMiner(m, 0, 1) as sm:
+            b = make_block(7, 3, 9, 1760572800, S1_PREV)
+            for d, rs in ((9, 0), (13, 5000), (17, 1 << 20), (13, 0)):
+                want = m.mine(b, 300, 1 << 24, d)
+                got = sm.mine(b, 300, 1 << 24, d, round_size=rs)
+                assert want is not None and got is not None and got.counter == want.counter
+                assert bytes(got.block.nonce) == bytes(want.block.nonce)
+                assert bytes(got.block.block_hash) == bytes(want.block.block_hash)
+            assert sm.mine(b, 0, 263, 9) is None  # golden: the first S1 solution is 263
     finally:
         dist.destroy_process_group()
+
+
+def _group_rank(rank, world, port, q, fault_rank):
+    """One rank of a multi-process group on the one GPU."""
+    import threading
+    import time
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if rank == fault_rank:
+        os.environ["POW_FAULT_INJECT"] = "mine"  # every pow_mine of this rank's context fails
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpi_blockchain_amd._lib import PowError
+    from mpi_blockchain_amd.miner import GpuMiner, block_hex
+    from mpi_blockchain_amd.shard import ShardedMiner
+
+    out = {}
+    S0 = make_block(1, 0, 9, 1700000000, b"")
+
+    def res(r):
+        return None if r is None else (r.counter, bytes(r.block.nonce).rstrip(b"\0").decode(), block_hex(r.block),
+                                       r.hashes)
+
+    with GpuMiner(0) as m:
+        m.warmup()
+        with ShardedMiner(m, rank, world) as sm:
+            if fault_rank >= 0:
+                try:
+                    sm.mine(S0, 0, 1 << 30, 21)
+                    out["fault"] = None
+                except PowError as e:
+                    out["fault"] = (e.code, str(e))
+            else:
+                # lowest mode: golden first solutions, adaptive rounds
+                out["d21"] = res(sm.mine(S0, 0, 1 << 26, 21))
+                out["d25"] = res(sm.mine(S0, 0, 1 << 28, 25))
+                # small unaligned fixed rounds (several rounds before the hit)
+                out["d13_rounds"] = res(sm.mine(S0, 300, 1 << 20, 13, round_size=1000 * world + 7))
+                # nothing in range: every rank returns None
+                out["none"] = res(sm.mine(S0, 0, 238, 9))
+                # any-mode: one agreed solving counter
+                r = sm.mine(S0, 0, 1 << 40, 28, any_solution=True)
+                out["any"] = res(r)
+                out["any_solves"] = r is not None and m.mine(S0, r.counter, 1, 28) is not None
+                # cancellation on ONE rank (mid-search, in-flight) stops every rank;
+                # the epoch is taken before the timer can move it
+                ep = m.epoch
+                if rank == world - 1:
+                    threading.Timer(0.2, m.cancel).start()
+                t = time.perf_counter()
+                out["cancel"] = res(sm.mine(S0, 0, 1 << 36, 64, epoch=ep))
+                out["cancel_s"] = time.perf_counter() - t
+                # and the group still mines correctly afterwards
+                out["after_cancel"] = res(sm.mine(S0, 0, 1 << 26, 21))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_ranks(world, fault_rank=-1, timeout=240):
+    import torch.multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_group_rank, args=(r, world, port, q, fault_rank)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = dict(q.get(timeout=timeout) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_group_multiprocess(world):
+    """pow_group_mine / pow_group_mine_any with `world` peer processes (C++
+    rounds, stop board shared through POSIX shared memory, the 24-byte
+    consensus through gloo): every rank returns the golden lowest counter with
+    its nonce and hash; any-mode agrees on one solving counter; one rank's
+    cancel makes every rank return None."""
+    from mpi_blockchain_amd.block import nonce_from_counter, solves_problem
+
+    out = _run_ranks(world)
+    for key, ctr, d in (("d21", 2392323, 21), ("d25", 73523910, 25), ("d13_rounds", 6399, 13)):
+        vals = {out[r][key][:3] for r in range(world)}
+        assert len(vals) == 1, (key, vals)  # the same result on every rank
+        c, nonce, hx = vals.pop()
+        assert c == ctr and nonce == nonce_from_counter(ctr).rstrip(b"\0").decode(), (key, c, nonce)
+        assert solves_problem(hx, d) and not solves_problem(hx, 64)
+    assert all(out[r]["none"] is None for r in range(world))
+    anys = {out[r]["any"][:3] for r in range(world)}
+    assert len(anys) == 1 and all(out[r]["any_solves"] for r in range(world))
+    assert all(out[r]["cancel"] is None for r in range(world))
+    # the first round is 2^30 counters per rank (~0.13 s alone, world x that on one
+    # shared GPU); the whole 2^36 range would take ~8 s
+    assert all(out[r]["cancel_s"] < 0.5 + 0.3 * world for r in range(world)), [out[r]["cancel_s"] for r in out]
+    assert all(out[r]["after_cancel"][0] == 2392323 for r in range(world))
+
+
+def test_group_failure_propagates():
+    """An injected failure on one rank (POW_FAULT_INJECT=mine: its pow_mine
+    returns POW_EHIP) makes every rank's pow_group_mine fail together: the
+    failing rank with its own error, its peers with POW_ECOMM."""
+    from mpi_blockchain_amd._lib import POW_ECOMM, POW_EHIP
+
+    world = 2
+    out = _run_ranks(world, fault_rank=1)
+    assert out[1]["fault"][0] == POW_EHIP and "injected fault" in out[1]["fault"][1]
+    assert out[0]["fault"][0] == POW_ECOMM and "a peer rank failed" in out[0]["fault"][1]
 
 
 def test_native_group_world1():
@@ -90,58 +216,6 @@ def test_native_group_from_torch():
             assert r is not None and r.counter == 238  # golden: first S0 solution
     finally:
         dist.destroy_process_group()
-
-
-def _board_rank(rank, world, port, q):
-    import torch.distributed as dist
-
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), POW_GRID_PER_CU="4")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mpi_blockchain_amd.miner import GpuMiner
-    from mpi_blockchain_amd.shard import ShardedMiner
-
-    out = {}
-    with GpuMiner(0) as m:
-        m.warmup()
-        sm = ShardedMiner(m, rank, world, board=True)
-        b = make_block(1, 0, 9, 1700000000, b"")
-        # lowest mode: S0's first d = 21 solution (golden) lies in rank 0's shard of
-        # the first 2^26-counter round; rank 1's shard stops on rank 0's hit
-        out["lowest"] = sm.mine(b, 0, 1 << 26, 21, round_size=1 << 26)
-        # any-mode: the first solution either rank finds; both agree on it
-        out["any"] = sm.mine(b, 0, 1 << 40, 28, any_solution=True)
-        out["any_solves"] = m.mine(b, out["any"], 1, 28) is not None if out["any"] is not None else False
-        sm.close()
-    q.put((rank, out))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_sharded_board_two_ranks():
-    """Two processes share this GPU (gloo; RCCL would refuse two ranks on one
-    device), each a ShardedMiner rank with a named stop board: the lowest
-    counter is the golden one on both ranks, and an any-mode search ends
-    with one agreed, solving counter."""
-    import torch.multiprocessing as mp
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_board_rank, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    try:
-        out = dict(q.get(timeout=180) for _ in procs)
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-    assert all(p.exitcode == 0 for p in procs)
-    assert out[0]["lowest"] == out[1]["lowest"] == 2392323
-    assert out[0]["any"] == out[1]["any"] is not None
-    assert out[0]["any_solves"] and out[1]["any_solves"]
 
 
 def test_native_group_beside_torch_rccl():
