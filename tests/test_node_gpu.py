@@ -12,7 +12,7 @@ import pytest
 
 from helpers import check_chain
 from mpi_blockchain_amd.build import mpi_available
-from mpi_blockchain_amd.node import run_network
+from mpi_blockchain_amd.node import chain_status, run_network
 
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not mpi_available(), reason="no MPI in this image")]
@@ -32,7 +32,10 @@ def test_gpu_network(tmp_path, np_, d):
     # GPU set-up in pow_node's main).  At d = 5 the fork is forced rather
     # than left to timing: --hold-first makes every rank mine block 1 and
     # publish it only after a barrier, so every rank receives rival blocks 1.
-    extra = ("--hold-first", "1") if d <= 5 else ()
+    # --winner-pause-us 3000: a block's finder waits 3 ms before mining the
+    # next, so the losers' chain migrations finish before the finder (~20 us
+    # per block at d = 5) completes the chain and MPI_Abort ends the job.
+    extra = ("--hold-first", "1", "--winner-pause-us", "3000") if d <= 5 else ()
     t0 = time.perf_counter()
     run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240, extra_args=extra)
     if os.environ.get("POW_NODE_LOG_DIR"):  # diagnostics: keep the network's output
@@ -47,26 +50,39 @@ def test_gpu_network(tmp_path, np_, d):
         # every rank mined its own block 1 before anyone published one
         assert len(re.findall(r"Agregué un producido con index 1 ", run.stdout)) == np_, run.stdout[-3000:]
         assert RIVAL_BLOCK1.search(run.stdout), run.stdout[-3000:]
+        # ... and a chain migration (verificar_y_migrar_cadena, node.cpp:152-191)
+        # that requested, checked and spliced a peer's branch
+        assert MIGRATED.search(run.stdout), run.stdout[-3000:]
 
 
-@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference binary not built")
-def test_mixed_with_reference_nodes(tmp_path):
-    """2 reference ranks (picosha2, CPU) + 2 GPU ranks in one mpiexec at the
-    reference's DEFAULT_DIFFICULTY (9): the reference ranks validate and adopt
-    GPU-mined blocks, the GPU ranks validate the reference's."""
-    # --serial-init 1: GPU set-up before MPI_Init, so MPI_Init is every rank's
-    # start line as in the reference (reference ranks join no start barrier).
-    # --idle-below 3: the GPU ranks mine only once the chain holds block 3, so blocks 1-3
-    # come from the reference ranks and both directions of adoption are
-    # certain (with a timing knob alone, a slow box let the GPU ranks win all
-    # 10 blocks in 1 of 2 runs: profiles/r02/verify/protocol_soak_mixed_*.log).
-    run = run_network(2, str(tmp_path), difficulty=9, blocks=10, timeout=240, ref_binary=REF_BIN, n_ref=2,
-                      extra_args=("--serial-init", "1", "--idle-below", "3"))
-    assert run.returncode == 0, run.stdout[-3000:]
-    assert "Error duro" not in run.stdout, run.stdout[-3000:]
-    # reference ranks 0/1 accepted blocks sent by GPU ranks 2/3
-    adopted = re.findall(r"\[(\d)\] Agregado a la lista bloque con index \d+ enviado por (\d)", run.stdout)
-    assert any(int(r) < 2 and int(s) >= 2 for r, s in adopted), run.stdout[-3000:]
-    # and GPU ranks accepted blocks mined by the reference (validated by K2)
-    assert any(int(r) >= 2 and int(s) < 2 for r, s in adopted), run.stdout[-3000:]
-    assert [r for r, entries in run.chains.items() if check_chain(entries, 10, 9)]
+# node.cpp:176: the splice of a checked chain; i >= 0 is the common ancestor's slot
+MIGRATED = re.compile(r"\[(\d+)\]: find = (\d+) \| received_blockchain_checks = 1")
+
+
+@pytest.mark.parametrize("np_", [2, 4])
+def test_mutual_chain_request(tmp_path, np_):
+    """the reference blocks in MPI_Recv(TAG_CHAIN_RESPONSE)
+    while holding the mutex its receive loop needs (node.cpp:155-161,
+    404-405), so two ranks that request each other's chains deadlock.  With
+    --private-lead 3 (pow_node_test) every rank mines blocks 1..3 on a private
+    branch and all publish their tips at once: every rank is 3 behind ("Perdí
+    la carrera por varios"), asks the tip's owner for its chain while that
+    owner asks it, serves the owner's TAG_CHAIN_HASH inside its own wait,
+    receives the chain, checks it and splices it in (find = 2: block 1 is the
+    common point with genesis).  The network then finishes its 10 blocks."""
+    run = run_network(np_, str(tmp_path), difficulty=9, blocks=10, timeout=120, extra_args=("--private-lead", "3"))
+    out = run.stdout
+    assert run.returncode == 0, out[-3000:]
+    assert "Error duro" not in out, out[-3000:]
+    for r in range(np_):
+        assert len(re.findall(rf"\[{r}\] Bloque privado con index \d ", out)) == 3, out[-3000:]
+        assert f"[{r}] Perdí la carrera por varios contra" in out, out[-3000:]
+        assert f"[{r}]: find = 2 | received_blockchain_checks = 1" in out, out[-3000:]
+    served = re.findall(r"\[(\d+)\] TAG_CHAIN_HASH de (\d+) atendido mientras espero la cadena de (\d+)", out)
+    if np_ == 2:  # each rank served its peer's request while waiting for that same peer's chain
+        assert {(int(a), int(b), int(c)) for a, b, c in served} >= {(0, 1, 1), (1, 0, 0)}, out[-3000:]
+    else:
+        assert served, out[-3000:]
+    # the rank that completes the chain dumps it and aborts the job (node.cpp:286-290, 330)
+    st = [chain_status(c, 10, 9) for c in run.chains.values()]
+    assert st and all(ok for ok, _ in st) and any(done for _, done in st), out[-3000:]
