@@ -186,12 +186,17 @@ __device__ __forceinline__ bool full_test(const uint32_t H[8], uint32_t d) {
 
 }  // namespace
 
+#define POW_BATCH 8u  // chunks claimed per global atomic (one workgroup's batch)
+
 // Work distribution: each wave dequeues chunks of 64 consecutive prefixes (one
-// per lane) from res->next with one atomic, in increasing order.  Any grid
+// per lane) in increasing order, through its workgroup's batches of POW_BATCH
+// chunks (one global atomic on res->next per batch).  Any grid
 // size and residency gives a tail of at most one chunk per wave (~2 ms), and
 // mine mode stays exact: a wave stops only when the lowest solution already
 // found is below its next chunk, and every lower chunk is owned by a wave
-// that is still running it.
+// that is still running it or still sits in a workgroup's batch (a batch's
+// chunks are handed out in increasing order, so a workgroup whose wave saw its
+// next chunk above the solution holds no lower one).
 // 80 SGPRs: the measured admission rule for 256-thread workgroups on gfx950
 // (MI355X_MICROARCH.md "Residency") gives 8 per CU only at <= 80; at the
 // compiler's natural ~92 it is 7.
@@ -214,12 +219,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
   __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
   lkw[threadIdx.x] = (&C->kw[0][0])[threadIdx.x];
   __shared__ uint32_t sibs_done;  // mine modes, workgroup 0: waves 1..3 that have finished (see the exit)
-  if (threadIdx.x == 0) sibs_done = 0;
+  __shared__ uint32_t wg_tick;                  // dequeue tickets of this workgroup
+  __shared__ unsigned long long wg_ring[4];     // (batch + 1) << 32 | base of the batch's first chunk
+  if (threadIdx.x == 0) {
+    sibs_done = 0;
+    wg_tick = 0;
+  }
+  if (threadIdx.x < 4) wg_ring[threadIdx.x] = 0;
   __syncthreads();
 
   for (;;) {
+    // Dequeue one 64-prefix chunk.  Tickets come from an LDS counter: ticket
+    // t is chunk t % POW_BATCH of the workgroup's batch t / POW_BATCH, and the
+    // wave holding a batch's first ticket claims the whole batch (POW_BATCH
+    // chunks) with ONE global atomic and publishes its base in a 4-slot LDS
+    // ring tagged with the batch number; the batch's other waves read it there
+    // (at most 4 waves hold one ticket each, so a slot is not reused while
+    // read).  Chunks are still handed out one per wave in increasing order
+    // within a workgroup, and batches in increasing order across the grid.
+    // 8 chunks per atomic: WRITE_SIZE 73.2 -> 42.7 MB per 2^32 window (the
+    // atomics were ~37 MB of it) at equal speed (profiles/r03/ab/ab4_*).
     uint32_t got = 0;
-    if (lane == 0) got = atomicAdd(&res->next, 64u);
+    if (lane == 0) {
+      const uint32_t t = atomicAdd(&wg_tick, 1u);
+      const uint32_t b = t / POW_BATCH, slot = t % POW_BATCH;
+      unsigned long long* const ring = &wg_ring[b & 3u];
+      if (slot == 0) {
+        got = atomicAdd(&res->next, 64u * POW_BATCH);
+        __hip_atomic_store(ring, ((unsigned long long)(b + 1u) << 32) | got, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        unsigned long long v;
+        while ((uint32_t)((v = __hip_atomic_load(ring, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) !=
+               b + 1u)
+          __builtin_amdgcn_s_sleep(1);
+        got = (uint32_t)v + 64u * slot;
+      }
+    }
     const uint32_t rbase = __builtin_amdgcn_readfirstlane(got);
     if (rbase >= L.n_prefix) break;
     if (MODE >= 1) {
@@ -303,6 +339,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       cptr J = pin(Cb, s2.a ^ j);  // per-j words and the chunk-0 uniform terms
       const uint32_t kw3 = J[PC_KW3 + j];
       St s{A3 + kw3, s2.a, s2.b, s2.c, E3 + kw3, s2.e, s2.f, s2.g};
+      // Code placement: the trial block runs ~1.1% faster when it starts on an
+      // 8-byte boundary than 4 bytes past one (same instructions; A/B in one
+      // process, profiles/r03/ab/ab3_code_placement.log: 498.3 vs 504.0 ms per
+      // 2^32 window).  The alignment pins that phase whatever code precedes the
+      // loop; it costs at most one s_nop per trial (tests/test_build.py).
+      asm volatile(".p2align 3");
       // Every round in round_ordered's issue order (sha256_dev.h); each
       // schedule word is computed just before its round (computing it one
       // round earlier measured 0.9% slower, profiles/r02/ab/ab8).

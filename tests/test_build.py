@@ -160,3 +160,18 @@ def test_valu_microbench_streams():
         c = collections.Counter(o.split()[0] for o in ops)
         assert set(c) == kinds and len(set(c.values())) == 1, (k, c)  # equal counts: one of each per step
         assert not [o for o in ops if re.search(r"\bs\d+\b|\bs\[", o)], k
+
+
+@pytest.mark.parametrize("variant", ["_Z10pow_searchILi0ELb0E", "_Z10pow_searchILi1ELb0E", "_Z10pow_searchILi2ELb0E",
+                                     "_Z10pow_searchILi0ELb1E"])
+def test_trial_block_phase_pinned(isa, variant):
+    """The trial block starts on an 8-byte boundary (.p2align 3 at its head):
+    the same block 4 bytes off that phase ran ~1.1% slower
+    (profiles/r03/ab/ab3_code_placement.log), and the phase would otherwise
+    follow whatever code precedes the loop.  The padding is at most one
+    4-byte s_nop per trial."""
+    body = j_loop_body(isa, variant)
+    assert body.count(".p2align 3") == 1, body.count(".p2align 3")
+    head = body.split(".p2align 3")[0]
+    # the directive sits at the head of the block: only the per-j scalar set-up precedes it
+    assert len(re.findall(r"^\s+v_", head, flags=re.M)) <= 8, head[-2000:]
