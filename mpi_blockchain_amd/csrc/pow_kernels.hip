@@ -56,20 +56,44 @@ __device__ __forceinline__ cptr pin(cptr p, uint32_t dep) {
 }
 
 // 64 rounds of a chunk whose K+W are template constants (chunks 1-4, K1 and
-// K1'): the K+W words come from LDS (a per-workgroup copy of C->kw) into VGPRs, 4 per ds_read_b128 (every lane reads the same address:
-// a broadcast), so the K+W add has two VGPR operands.  A VALU op with an SGPR
+// K1'): the K+W words come from LDS (a per-workgroup copy of C->kw) into
+// VGPRs, 4 per ds_read_b128 (every lane reads the same address: a
+// broadcast), so the K+W add has two VGPR operands.  A VALU op with an SGPR
 // operand issues at half rate on gfx950; moving these 256 adds
 // per trial off SGPRs made the sweep 0.7% faster (profiles/r02/ab/).  Chunk
 // 0's K and K+W words stay scalar loads: its SGPR operands sit in v_add3
 // (half rate anyway), and LDS copies of them measured 0.4-0.6% slower.
+//
+// ASM (K1): each group of 4 rounds is one asm block of 8-byte instructions
+// held 4 bytes past an 8-byte boundary (sha256_dev.h rounds4_asm): 4.1% less
+// kernel time than the compiler's mix of 4- and 8-byte encodings, whose phase
+// flipped at every 4-byte instruction (profiles/r03/ab/ab8_*).  K1' (one wave
+// per SIMD at low d) keeps the compiler's rounds: its time-to-block at d = 13
+// went from 0.034 to 0.038 ms with the asm groups.
+template <bool ASM>
 __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
+  if (ASM) {
+    POW_SB();
+    const uint4 v0 = *reinterpret_cast<const uint4*>(lkw);
+    POW_SB();
+    t = rounds4_asm_from(t, v0.x, v0.y, v0.z, v0.w);
 #pragma unroll
-  for (int g = 0; g < 64; g += 4) {
-    const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
-    round_kw_o(t, v.x);
-    round_kw_o(t, v.y);
-    round_kw_o(t, v.z);
-    round_kw_o(t, v.w);
+    for (int g = 4; g < 64; g += 4) {
+      POW_SB();
+      const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
+      POW_SB();
+      rounds4_asm(t, v.x, v.y, v.z, v.w);
+    }
+    POW_SB();
+  } else {
+#pragma unroll
+    for (int g = 0; g < 64; g += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
+      round_kw_o(t, v.x);
+      round_kw_o(t, v.y);
+      round_kw_o(t, v.z);
+      round_kw_o(t, v.w);
+    }
   }
 }
 
@@ -391,13 +415,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-        const_chunk_lds(t, lkw + 64 * c);
+        const_chunk_lds<true>(t, lkw + 64 * c);
         H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
         H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
       }
       // ---------------- chunk 4 (last): only what the test needs ----------------
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk_lds(t, lkw + 64 * 3);
+      const_chunk_lds<true>(t, lkw + 64 * 3);
       const uint32_t h0 = H[0] + t.a;
 
       bool hit = h0 <= L.thr;
@@ -593,12 +617,12 @@ __global__ __launch_bounds__(256) void pow_search_lat(
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk_lds(t, lk + 64 * c);
+      const_chunk_lds<false>(t, lk + 64 * c);
       H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
       H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
     }
     St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-    const_chunk_lds(t, lk + 64 * 3);
+    const_chunk_lds<false>(t, lk + 64 * 3);
     // The whole digest stays live here (this kernel runs at <= 4 waves/SIMD,
     // so the 7 extra VGPRs cost no residency): a hit records it, and the
     // winner's block_hash needs no K2 launch (one serial SHA-256 of 5 chunks

@@ -90,6 +90,69 @@ __device__ __forceinline__ void round_ordered(St& s, uint32_t k, uint32_t w) {
 __device__ __forceinline__ void round_kw_o(St& s, uint32_t kw) { round_ordered<false>(s, kw, 0u); }
 __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { round_ordered<true>(s, k, w); }
 
+// Four rounds of a constant-schedule chunk (K+W from LDS) as ONE asm block:
+// 56 VALU instructions, every one 8 bytes long (v_add_u32_e64, never the
+// 4-byte VOP2 form hipcc picks), in the order hipcc emitted round_ordered.
+// Each block starts with `.p2align 3; s_nop 0`, so every VALU instruction of
+// a chunk sits 4 bytes past an 8-byte boundary whatever the compiler puts
+// before the block (its s_waitcnt for the LDS words, a hazard s_nop): on
+// gfx950 that phase issues ~5% faster than the other for this stream
+// (tools/place_probe*.hip, profiles/r03/probe/).
+//   POW_RX(a, b, c, d, e, f, g, h, d', h', KW): one round reading a..h and
+//   writing e' into d' and a' into h' (d' = d, h' = h for in-place).
+#define POW_RX(a, b, c, d, e, f, g, h, dd, hh, KW)                     \
+  "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"             \
+  "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"             \
+  "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                           \
+  "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                          \
+  "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                          \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                           \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                          \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                          \
+  "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"             \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"             \
+  "\tv_add_u32_e64 " hh ", " h ", " KW "\n"                             \
+  "\tv_add3_u32 " hh ", " hh ", %[t5], %[t0]\n"                         \
+  "\tv_add_u32_e64 " dd ", " d ", " hh "\n"                             \
+  "\tv_add3_u32 " hh ", " hh ", %[t2], %[t1]\n"
+#define POW_R(a, b, c, d, e, f, g, h, KW) POW_RX(a, b, c, d, e, f, g, h, d, h, KW)
+#define POW_PHASE "\t.p2align 3\n\ts_nop 0\n"
+#define POW_TEMPS                                                                                    \
+  [t0] "=&v"(x0), [t1] "=&v"(x1), [t2] "=&v"(x2), [t3] "=&v"(x3), [t4] "=&v"(x4), [t5] "=&v"(x5),   \
+      [t6] "=&v"(x6), [t7] "=&v"(x7)
+// In place: the state is read and written in the same registers.
+__device__ __forceinline__ void rounds4_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  asm volatile(POW_PHASE
+               POW_R("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]")
+               POW_R("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]")
+               POW_R("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]")
+               POW_R("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]")
+               : [a] "+v"(s.a), [b] "+v"(s.b), [c] "+v"(s.c), [d] "+v"(s.d), [e] "+v"(s.e), [f] "+v"(s.f),
+                 [g] "+v"(s.g), [h] "+v"(s.h), POW_TEMPS
+               : [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
+  // after four rounds the state sits in the registers of (e, f, g, h, a, b, c, d)
+  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
+}
+// A chunk's first four rounds: the input state (the chaining value H, still
+// needed for the feed-forward) is only read; each of the 8 state words is
+// written once, into a fresh register, so no copies of H are needed.
+__device__ __forceinline__ St rounds4_asm_from(const St& in, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  St o;
+  asm volatile(POW_PHASE
+               POW_RX("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[od]", "%[oh]", "%[k0]")
+               POW_RX("%[oh]", "%[a]", "%[b]", "%[c]", "%[od]", "%[e]", "%[f]", "%[g]", "%[oc]", "%[og]", "%[k1]")
+               POW_RX("%[og]", "%[oh]", "%[a]", "%[b]", "%[oc]", "%[od]", "%[e]", "%[f]", "%[ob]", "%[of]", "%[k2]")
+               POW_RX("%[of]", "%[og]", "%[oh]", "%[a]", "%[ob]", "%[oc]", "%[od]", "%[e]", "%[oa]", "%[oe]", "%[k3]")
+               : [oa] "=&v"(o.a), [ob] "=&v"(o.b), [oc] "=&v"(o.c), [od] "=&v"(o.d), [oe] "=&v"(o.e),
+                 [of] "=&v"(o.f), [og] "=&v"(o.g), [oh] "=&v"(o.h), POW_TEMPS
+               : [a] "v"(in.a), [b] "v"(in.b), [c] "v"(in.c), [d] "v"(in.d), [e] "v"(in.e), [f] "v"(in.f),
+                 [g] "v"(in.g), [h] "v"(in.h), [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
+  return St{o.e, o.f, o.g, o.h, o.a, o.b, o.c, o.d};
+}
+
+
 // Generic compression of one chunk (used by the single-hash kernel K2; not on
 // the mining hot loop).  The schedule is a 16-word ring computed just ahead
 // of its round, and scheduling barriers every 4 rounds keep the compiler from

@@ -168,10 +168,62 @@ def test_trial_block_phase_pinned(isa, variant):
     """The trial block starts on an 8-byte boundary (.p2align 3 at its head):
     the same block 4 bytes off that phase ran ~1.1% slower
     (profiles/r03/ab/ab3_code_placement.log), and the phase would otherwise
-    follow whatever code precedes the loop.  The padding is at most one
-    4-byte s_nop per trial."""
+    follow whatever code precedes the loop.  Chunks 1-4 then run as 64 asm
+    groups of 4 rounds, each pinned by its own .p2align 3 (1 + 64)."""
     body = j_loop_body(isa, variant)
-    assert body.count(".p2align 3") == 1, body.count(".p2align 3")
+    assert body.count(".p2align 3") == 65, body.count(".p2align 3")
     head = body.split(".p2align 3")[0]
-    # the directive sits at the head of the block: only the per-j scalar set-up precedes it
+    # the first directive sits at the head of the block: only the per-j scalar set-up precedes it
     assert len(re.findall(r"^\s+v_", head, flags=re.M)) <= 8, head[-2000:]
+
+
+@pytest.fixture(scope="module")
+def k1_code():
+    """(address, mnemonic, bytes) of K1's sweep kernel in the assembled gfx950
+    code object (the .s has no addresses)."""
+    from mpi_blockchain_amd.build import hipcc
+
+    with tempfile.TemporaryDirectory() as td:
+        co = os.path.join(td, "k.co")
+        subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-mcode-object-version=5",
+                        "-I", os.path.join(ROOT, "include"), "-I", CSRC, "--cuda-device-only",
+                        "--no-gpu-bundle-output", "-c", os.path.join(CSRC, "pow_kernels.hip"), "-o", co],
+                       check=True, cwd=td, capture_output=True)
+        dis = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", co], check=True, capture_output=True,
+                             text=True).stdout
+    lines = dis.splitlines()
+    fn = "_Z10pow_searchILi0ELb0EEvPK9PowConsts9PowLaunchPjP9PowResult"
+    i = [k for k, ln in enumerate(lines) if ln.endswith("<" + fn + ">:")][0]
+    end = next((k for k in range(i + 1, len(lines)) if re.match(r"^[0-9a-f]{16} <_Z", lines[k])), len(lines))
+    out = []
+    for ln in lines[i:end]:
+        m = re.match(r"^\s+(\S+).*//\s*([0-9A-Fa-f]+):\s*([0-9A-Fa-f ]+)$", ln)
+        if m:
+            out.append((int(m.group(2), 16), m.group(1), 4 * len(m.group(3).split())))
+    return out
+
+
+def test_chunk_rounds_keep_one_phase(k1_code):
+    """Chunks 1-4 (3,600 of a trial's ~4,840 VALU instructions): every
+    instruction of the 64 asm groups is 8 bytes long and starts 4 bytes past
+    an 8-byte boundary.  That phase issued ~5% faster in the probes
+    (tools/place_probe*.hip) and the groups 4.1% faster in K1
+    (profiles/r03/ab/ab8_asm_groups_chunks14.log) than hipcc's mixed
+    4/8-byte encodings, whose phase flipped at every 4-byte instruction."""
+    ds_all = [k for k, (a, op, sz) in enumerate(k1_code) if op == "ds_read_b128"]
+    # the trial's 64 reads: the longest run of ds_read_b128 one group (~60 instructions) apart
+    runs, cur = [], [ds_all[0]]
+    for k in ds_all[1:]:
+        if k - cur[-1] < 200:
+            cur.append(k)
+        else:
+            runs.append(cur)
+            cur = [k]
+    runs.append(cur)
+    # (the sweep's flush of staged solutions right after the trial reads LDS 16 B per lane too)
+    ds = max(runs, key=len)[:64]
+    assert len(ds) == 64, [len(r) for r in runs]
+    chunk = [x for x in k1_code[ds[0]:ds[-1] + 60] if x[1].startswith("v_")]
+    eight = [x for x in chunk if x[2] == 8]
+    off = [x for x in eight if x[0] % 8 != 4]
+    assert len(eight) >= 3584 and len(off) <= 32, (len(eight), len(off))
