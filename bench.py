@@ -450,12 +450,12 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
                     "hashes include the trials peers ran before the winner's hit reached them"}
 
 
-# Issue classes of one trial of K1's j-loop (4,838 VALU instructions, read from
+# Issue classes of one trial of K1's j-loop (4,839 VALU instructions, read from
 # the gfx950 ISA; tests/test_build.py checks these against the disassembly):
-# half rate = 2,046 v_alignbit_b32 + 720 v_add3_u32 + 9 otherwise full-rate ops
+# half rate = 2,046 v_alignbit_b32 + 719 v_add3_u32 + 9 otherwise full-rate ops
 # with an SGPR operand; full rate = v_bitop3_b32, v_add_u32, v_lshrrev_b32, ...
-TRIAL_HALF_RATE = 2775
-TRIAL_FULL_RATE = 2063
+TRIAL_HALF_RATE = 2774
+TRIAL_FULL_RATE = 2065
 
 
 def valu_peaks(miner, device: int, cu_count: int) -> dict:

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       cptr Cb = as_const(reinterpret_cast<const uint32_t*>(C));
       cptr J = pin(Cb, s2.a ^ j);  // per-j words and the chunk-0 uniform terms
       const uint32_t kw3 = J[PC_KW3 + j];
-      St s{A3 + kw3, s2.a, s2.b, s2.c, E3 + kw3, s2.e, s2.f, s2.g};
+      const St s4{A3 + kw3, s2.a, s2.b, s2.c, E3 + kw3, s2.e, s2.f, s2.g};
       // Code placement: the trial block runs ~1.1% faster when it starts on an
       // 8-byte boundary than 4 bytes past one (same instructions; A/B in one
       // process, profiles/r03/ab/ab3_code_placement.log: 498.3 vs 504.0 ms per
@@ -372,8 +372,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       // Every round in round_ordered's issue order (sha256_dev.h); each
       // schedule word is computed just before its round (computing it one
       // round earlier measured 0.9% slower, profiles/r02/ab/ab8).
+      POW_SB();
+      St s = rounds4_kws_asm_from(s4, J[PC_KW0 + 4], J[PC_KW0 + 5], J[PC_KW0 + 6], J[PC_KW0 + 7]);
 #pragma unroll
-      for (int i = 4; i < 16; ++i) round_kw_o(s, J[PC_KW0 + i]);
+      for (int i = 8; i < 16; i += 4) {
+        POW_SB();
+        rounds4_kws_asm(s, J[PC_KW0 + i], J[PC_KW0 + i + 1], J[PC_KW0 + i + 2], J[PC_KW0 + i + 3]);
+      }
       uint32_t w[64];
       w[16] = W16;
       w[17] = W17;
@@ -389,24 +394,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         else if (i == 32) w[32] = ssig1(w[30]) + w[25] + c32;
         else w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
       };
-      auto rnd = [&](int i, cptr Kx) {
-        if (i >= 18) wcalc(i);
-        round_k_w_o(s, Kx[i], w[i]);
+      // rounds i..i+3: their four schedule words first (compiler code), then
+      // the rounds as one asm group at the pinned phase
+      auto rnd4 = [&](int i, cptr Kx) {
+        if (i >= 36) {  // generic schedule words: computed inside the group
+          POW_SB();
+          uint32_t q[4] = {w[i - 16], w[i - 15], w[i - 14], w[i - 13]};
+          rounds4_sched_asm(s, Kx[i], Kx[i + 1], Kx[i + 2], Kx[i + 3], q, w[i - 12], &w[i - 7], w[i - 2], w[i - 1]);
+          w[i] = q[0];
+          w[i + 1] = q[1];
+          w[i + 2] = q[2];
+          w[i + 3] = q[3];
+          return;
+        }
+#pragma unroll
+        for (int q = i; q < i + 4; ++q)
+          if (q >= 18) wcalc(q);
+        POW_SB();
+        rounds4_ks_w_asm(s, Kx[i], Kx[i + 1], Kx[i + 2], Kx[i + 3], w[i], w[i + 1], w[i + 2], w[i + 3]);
       };
       {
         cptr Kp = pin(Cb + PC_K, s.e);  // K[16..63], streamed like the K+W words
 #pragma unroll
-        for (int i = 16; i < 32; ++i) rnd(i, Kp);
+        for (int i = 16; i < 32; i += 4) rnd4(i, Kp);
       }
       {
         cptr K2 = pin(Cb + PC_K, s.e);
 #pragma unroll
-        for (int i = 32; i < 48; ++i) rnd(i, K2);
+        for (int i = 32; i < 48; i += 4) rnd4(i, K2);
       }
       {
         cptr K3 = pin(Cb + PC_K, s.e);
 #pragma unroll
-        for (int i = 48; i < 64; ++i) rnd(i, K3);
+        for (int i = 48; i < 64; i += 4) rnd4(i, K3);
       }
       uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
                        IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};

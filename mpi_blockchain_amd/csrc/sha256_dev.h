@@ -120,6 +120,123 @@ __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { rou
 #define POW_TEMPS                                                                                    \
   [t0] "=&v"(x0), [t1] "=&v"(x1), [t2] "=&v"(x2), [t3] "=&v"(x3), [t4] "=&v"(x4), [t5] "=&v"(x5),   \
       [t6] "=&v"(x6), [t7] "=&v"(x7)
+// Chunk 0's rounds, K+W (or K) from SGPRs (scalar loads of the template
+// constants), W per lane.  The additions keep hipcc's forms (and rates):
+//   rounds 4-15, K+W uniform:  h' = h + Ch (full rate);  T1 = h' + S1 + KW (v_add3, SGPR)
+//   rounds 16-63, K uniform, W per lane: T1 = Ch + h + S1; T1 += K + W (two v_add3, SGPR)
+#define POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                         \
+  "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"           \
+  "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"           \
+  "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                         \
+  "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                        \
+  "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                        \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                         \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                        \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                        \
+  "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"           \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"
+#define POW_R_KWS(a, b, c, d, e, f, g, h, KWS)                          \
+  POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                               \
+  "\tv_add_u32_e64 " h ", " h ", %[t0]\n"                             \
+  "\tv_add3_u32 " h ", " h ", %[t5], " KWS "\n"                       \
+  "\tv_add_u32_e64 " d ", " d ", " h "\n"                             \
+  "\tv_add3_u32 " h ", %[t2], %[t1], " h "\n"
+#define POW_R_KS_W(a, b, c, d, e, f, g, h, KS, W)                       \
+  POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                               \
+  "\tv_add3_u32 " h ", %[t0], " h ", %[t5]\n"                         \
+  "\tv_add3_u32 " h ", " h ", " KS ", " W "\n"                        \
+  "\tv_add_u32_e64 " d ", " d ", " h "\n"                             \
+  "\tv_add3_u32 " h ", %[t2], %[t1], " h "\n"
+#define POW_STATE_OPS                                                                             \
+  [a] "+v"(s.a), [b] "+v"(s.b), [c] "+v"(s.c), [d] "+v"(s.d), [e] "+v"(s.e), [f] "+v"(s.f),        \
+      [g] "+v"(s.g), [h] "+v"(s.h)
+// Four chunk-0 rounds with uniform K+W words (SGPR operands).
+__device__ __forceinline__ void rounds4_kws_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  asm volatile(POW_PHASE
+               POW_R_KWS("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]")
+               POW_R_KWS("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]")
+               POW_R_KWS("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]")
+               POW_R_KWS("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]")
+               : POW_STATE_OPS, POW_TEMPS
+               : [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3));
+  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
+}
+// The same for rounds 4-7, reading the state entering round 4 (most of it
+// the per-prefix state, live across the j-loop) without writing it: each
+// state word is written once, into a fresh register (no copies).
+#define POW_R_KWS_X(a, b, c, d, e, f, g, h, dd, hh, KWS)                 \
+  POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                               \
+  "\tv_add_u32_e64 " hh ", " h ", %[t0]\n"                            \
+  "\tv_add3_u32 " hh ", " hh ", %[t5], " KWS "\n"                     \
+  "\tv_add_u32_e64 " dd ", " d ", " hh "\n"                           \
+  "\tv_add3_u32 " hh ", %[t2], %[t1], " hh "\n"
+__device__ __forceinline__ St rounds4_kws_asm_from(const St& in, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  St o;
+  asm volatile(POW_PHASE
+               POW_R_KWS_X("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[od]", "%[oh]", "%[k0]")
+               POW_R_KWS_X("%[oh]", "%[a]", "%[b]", "%[c]", "%[od]", "%[e]", "%[f]", "%[g]", "%[oc]", "%[og]", "%[k1]")
+               POW_R_KWS_X("%[og]", "%[oh]", "%[a]", "%[b]", "%[oc]", "%[od]", "%[e]", "%[f]", "%[ob]", "%[of]", "%[k2]")
+               POW_R_KWS_X("%[of]", "%[og]", "%[oh]", "%[a]", "%[ob]", "%[oc]", "%[od]", "%[e]", "%[oa]", "%[oe]", "%[k3]")
+               : [oa] "=&v"(o.a), [ob] "=&v"(o.b), [oc] "=&v"(o.c), [od] "=&v"(o.d), [oe] "=&v"(o.e),
+                 [of] "=&v"(o.f), [og] "=&v"(o.g), [oh] "=&v"(o.h), POW_TEMPS
+               : [a] "v"(in.a), [b] "v"(in.b), [c] "v"(in.c), [d] "v"(in.d), [e] "v"(in.e), [f] "v"(in.f),
+                 [g] "v"(in.g), [h] "v"(in.h), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3));
+  return St{o.e, o.f, o.g, o.h, o.a, o.b, o.c, o.d};
+}
+// Four chunk-0 rounds with uniform K (SGPR) and per-lane W.
+__device__ __forceinline__ void rounds4_ks_w_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
+                                                 uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  asm volatile(POW_PHASE
+               POW_R_KS_W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]", "%[w0]")
+               POW_R_KS_W("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]", "%[w1]")
+               POW_R_KS_W("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]", "%[w2]")
+               POW_R_KS_W("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]", "%[w3]")
+               : POW_STATE_OPS, POW_TEMPS
+               : [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3), [w0] "v"(w0), [w1] "v"(w1),
+                 [w2] "v"(w2), [w3] "v"(w3));
+  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
+}
+
+// A schedule word of chunk 0 (i >= 33): W = s1(W[i-2]) + W[i-7] + s0(W[i-15]) + W[i-16],
+// every instruction 8 bytes (v_lshrrev_b32_e64).  Uses t0..t3.
+#define POW_W(dst, wm2, wm7, wm15, wm16)                                \
+  "\tv_alignbit_b32 %[t0], " wm2 ", " wm2 ", 17\n"                    \
+  "\tv_alignbit_b32 %[t1], " wm2 ", " wm2 ", 19\n"                    \
+  "\tv_lshrrev_b32_e64 %[t2], 10, " wm2 "\n"                          \
+  "\tv_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n"           \
+  "\tv_alignbit_b32 %[t1], " wm15 ", " wm15 ", 7\n"                   \
+  "\tv_alignbit_b32 %[t2], " wm15 ", " wm15 ", 18\n"                  \
+  "\tv_lshrrev_b32_e64 %[t3], 3, " wm15 "\n"                          \
+  "\tv_bitop3_b32 %[t1], %[t1], %[t2], %[t3] bitop3:0x96\n"           \
+  "\tv_add3_u32 %[t0], %[t0], " wm7 ", %[t1]\n"                       \
+  "\tv_add_u32_e64 " dst ", %[t0], " wm16 "\n"
+// Four chunk-0 rounds i..i+3 (i >= 36) with their schedule words computed in
+// the same block, each just before its round.  W[i+k] is written over
+// W[i-16+k] (dead once W[i+k] is formed; POW_W reads its W[i-16] last), so the
+// block needs no registers beyond the window: w[0..3] = W[i-16..i-13] in,
+// W[i..i+3] out; w4 = W[i-12], v7[k] = W[i-7+k], m2 = W[i-2], m1 = W[i-1].
+__device__ __forceinline__ void rounds4_sched_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
+                                                  uint32_t* w, uint32_t w4, const uint32_t* v7, uint32_t m2,
+                                                  uint32_t m1) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  asm volatile(POW_PHASE
+               POW_W("%[o0]", "%[m2]", "%[v0]", "%[o1]", "%[o0]")
+               POW_R_KS_W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]", "%[o0]")
+               POW_W("%[o1]", "%[m1]", "%[v1]", "%[o2]", "%[o1]")
+               POW_R_KS_W("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]", "%[o1]")
+               POW_W("%[o2]", "%[o0]", "%[v2]", "%[o3]", "%[o2]")
+               POW_R_KS_W("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]", "%[o2]")
+               POW_W("%[o3]", "%[o1]", "%[v3]", "%[w4]", "%[o3]")
+               POW_R_KS_W("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]", "%[o3]")
+               : POW_STATE_OPS, POW_TEMPS, [o0] "+v"(w[0]), [o1] "+v"(w[1]), [o2] "+v"(w[2]), [o3] "+v"(w[3])
+               : [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3), [w4] "v"(w4), [v0] "v"(v7[0]),
+                 [v1] "v"(v7[1]), [v2] "v"(v7[2]), [v3] "v"(v7[3]), [m2] "v"(m2), [m1] "v"(m1));
+  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
+}
+
 // In place: the state is read and written in the same registers.
 __device__ __forceinline__ void rounds4_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;

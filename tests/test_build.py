@@ -168,10 +168,11 @@ def test_trial_block_phase_pinned(isa, variant):
     """The trial block starts on an 8-byte boundary (.p2align 3 at its head):
     the same block 4 bytes off that phase ran ~1.1% slower
     (profiles/r03/ab/ab3_code_placement.log), and the phase would otherwise
-    follow whatever code precedes the loop.  Chunks 1-4 then run as 64 asm
-    groups of 4 rounds, each pinned by its own .p2align 3 (1 + 64)."""
+    follow whatever code precedes the loop.  The rounds then run as asm
+    groups of 4, each pinned by its own .p2align 3: chunk 0's rounds 4-63 (15
+    groups) and chunks 1-4 (64 groups), 1 + 15 + 64 in all."""
     body = j_loop_body(isa, variant)
-    assert body.count(".p2align 3") == 65, body.count(".p2align 3")
+    assert body.count(".p2align 3") == 80, body.count(".p2align 3")
     head = body.split(".p2align 3")[0]
     # the first directive sits at the head of the block: only the per-j scalar set-up precedes it
     assert len(re.findall(r"^\s+v_", head, flags=re.M)) <= 8, head[-2000:]
