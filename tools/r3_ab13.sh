@@ -2,4 +2,4 @@ set -e
 R=$GRAFT_REPO_ROOT
 S=$R/tools/gpu_step.sh
 cd /tmp && export TMPDIR=/tmp
-$S pattern_probe 300 $R/tools/pattern_probe
+$S pattern_probe2 300 $R/tools/pattern_probe
