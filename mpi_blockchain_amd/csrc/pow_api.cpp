@@ -51,8 +51,8 @@ hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t str
 hipError_t pow_launch_hash(uint32_t n, hipStream_t stream, const uint32_t* msgs, uint32_t* digests);
 hipError_t pow_sort_u32(void* temp, size_t* temp_bytes, uint32_t* keys, uint32_t* alt, uint32_t n,
                         uint32_t** sorted, hipStream_t stream);
-hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream, const PowConstsLat& C,
-                                 const PowLaunchLat& L, PowResult* res, PowResult* hout);
+hipError_t pow_launch_search_lat(bool full, bool any, bool asm_groups, unsigned grid, hipStream_t stream,
+                                 const PowConstsLat& C, const PowLaunchLat& L, PowResult* res, PowResult* hout);
 
 namespace {
 
@@ -347,8 +347,13 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   L.seq = ctx->lat_seq;
   // One dispatch: constants by value (kernarg), result published by the
   // kernel's last wave into mapped host memory (no copy kernels), `done` last.
-  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, grid, ctx->stream, ctx->lat_consts, L,
-                               ctx->d_lat, ctx->d_lat_host));
+  // At 4+ waves per SIMD (d = 20, 21) chunks 1-4 run as K1's asm groups
+  // (8-byte encodings at the pinned phase): time-to-block at d = 21 0.220 ->
+  // 0.212 ms.  At 1-2 waves per SIMD the kernel is latency-bound and the
+  // compiler's interleaving of independent ops serves it better (d = 13:
+  // 0.034 -> 0.038 ms with the groups; profiles/r03/ab/ab8_*).
+  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, ctx->stream,
+                               ctx->lat_consts, L, ctx->d_lat, ctx->d_lat_host));
   // Return as soon as the result is published: the kernel's completion
   // signal reaches the host ~5 us after its last wave exits (rocprofv3 trace
   // of tools/ttb_c).  A launch that ends without publishing
@@ -557,8 +562,9 @@ int pow_warmup(pow_ctx* ctx) {
       HIP_OK(pow_launch_search(mode, full != 0, 1, ctx->stream, ctx->d_consts, L, nullptr, ctx->d_res));
   for (int any = 0; any < 2; ++any)
     for (int full = 0; full < 2; ++full)
-      HIP_OK(pow_launch_search_lat(full != 0, any != 0, 1, ctx->stream, ctx->lat_consts, LL, ctx->d_lat,
-                                   ctx->d_lat_host));
+      for (int grp = 0; grp < 2; ++grp)
+        HIP_OK(pow_launch_search_lat(full != 0, any != 0, grp != 0, 1, ctx->stream, ctx->lat_consts, LL,
+                                     ctx->d_lat, ctx->d_lat_host));
   HIP_OK(pow_launch_hash(0, ctx->stream, nullptr, nullptr));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   pow_block b;

@@ -97,6 +97,24 @@ __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
   }
 }
 
+// Chunks 2-4 (K1): the previous chunk's feed-forward H += t and this chunk's
+// first four rounds as one group (rounds4_asm_ff), then 15 groups as above;
+// t ends as this chunk's final state.
+__device__ __forceinline__ void const_chunk_lds_ff(St& H, St& t, const uint32_t* lkw) {
+  POW_SB();
+  const uint4 v0 = *reinterpret_cast<const uint4*>(lkw);
+  POW_SB();
+  rounds4_asm_ff(H, t, v0.x, v0.y, v0.z, v0.w);
+#pragma unroll
+  for (int g = 4; g < 64; g += 4) {
+    POW_SB();
+    const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
+    POW_SB();
+    rounds4_asm(t, v.x, v.y, v.z, v.w);
+  }
+  POW_SB();
+}
+
 // Append the 32-entry-aligned part of a wave's staged solutions (nst <= 127,
 // in LDS) to the global list with one atomic; the remainder (< 32) moves to
 // the stage front.  Every reservation is a multiple of 32 entries, so each
@@ -238,7 +256,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
   __shared__ __attribute__((aligned(16))) uint32_t stage[4][128];
   uint32_t* wst = stage[threadIdx.x >> 6];
   uint32_t nst = 0;                     // staged entries (wave-uniform)
-  unsigned long long mymin = ~0ull;     // lowest solution of this lane
+  // lowest solution of this lane, 32-bit (a sweep window is <= 2^32 counters,
+  // so rel < 2^32): one VGPR, not two (the 64-bit form spilled to scratch once
+  // the chunk-0 schedule moved into the asm groups).  0xFFFFFFFF means none; a
+  // solution AT rel = 0xFFFFFFFF goes straight to res->min_rel (at most once).
+  uint32_t mymin = 0xFFFFFFFFu;
   // chunks 1-4's K+W words, one per thread (blockDim = 256 = 4 x 64)
   __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
   lkw[threadIdx.x] = (&C->kw[0][0])[threadIdx.x];
@@ -382,20 +404,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       uint32_t w[64];
       w[16] = W16;
       w[17] = W17;
-      // schedule word i (template-uniform and per-prefix terms folded)
-      auto wcalc = [&](int i) {
-        if (i == 18) w[18] = c18 + J[PC_U18 + j];
-        else if (i == 19) w[19] = c19 + J[PC_W3 + j];
-        else if (i <= 22) w[i] = ssig1(w[i - 2]) + J[PC_U20 + i - 20];
-        else if (i == 23) w[23] = ssig1(w[21]) + c23;
-        else if (i == 24) w[24] = ssig1(w[22]) + c24;
-        else if (i <= 30) w[i] = ssig1(w[i - 2]) + w[i - 7] + J[PC_U25 + i - 25];
-        else if (i == 31) w[31] = ssig1(w[29]) + w[24] + c31;
-        else if (i == 32) w[32] = ssig1(w[30]) + w[25] + c32;
-        else w[i] = ssig1(w[i - 2]) + w[i - 7] + ssig0(w[i - 15]) + w[i - 16];
-      };
-      // rounds i..i+3: their four schedule words first (compiler code), then
-      // the rounds as one asm group at the pinned phase
+      // rounds i..i+3 with their four schedule words, as one asm group at the
+      // pinned phase (template-uniform and per-prefix terms folded)
       auto rnd4 = [&](int i, cptr Kx) {
         if (i >= 36) {  // generic schedule words: computed inside the group
           POW_SB();
@@ -407,11 +417,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
           w[i + 3] = q[3];
           return;
         }
-#pragma unroll
-        for (int q = i; q < i + 4; ++q)
-          if (q >= 18) wcalc(q);
+        // rounds 16-35: the folded schedule words (wcalc's forms) inside the groups
         POW_SB();
-        rounds4_ks_w_asm(s, Kx[i], Kx[i + 1], Kx[i + 2], Kx[i + 3], w[i], w[i + 1], w[i + 2], w[i + 3]);
+        if (i == 16)
+          rounds4_w_asm<0>(s, Kx[16], Kx[17], Kx[18], Kx[19], w, J[PC_U18 + j], J[PC_W3 + j], 0u, c18, c19);
+        else if (i == 20)
+          rounds4_w_asm<1>(s, Kx[20], Kx[21], Kx[22], Kx[23], w, J[PC_U20], J[PC_U20 + 1], J[PC_U20 + 2], c23, 0u);
+        else if (i == 24)
+          rounds4_w_asm<2>(s, Kx[24], Kx[25], Kx[26], Kx[27], w, J[PC_U25], J[PC_U25 + 1], J[PC_U25 + 2], c24, 0u);
+        else if (i == 28)
+          rounds4_w_asm<3>(s, Kx[28], Kx[29], Kx[30], Kx[31], w, J[PC_U25 + 3], J[PC_U25 + 4], J[PC_U25 + 5], c31,
+                           0u);
+        else
+          rounds4_w_asm<4>(s, Kx[32], Kx[33], Kx[34], Kx[35], w, 0u, 0u, 0u, c32, 0u);
       };
       {
         cptr Kp = pin(Cb + PC_K, s.e);  // K[16..63], streamed like the K+W words
@@ -431,23 +449,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       uint32_t H[8] = {IV[0] + s.a, IV[1] + s.b, IV[2] + s.c, IV[3] + s.d,
                        IV[4] + s.e, IV[5] + s.f, IV[6] + s.g, IV[7] + s.h};
 
-      // ---------------- chunks 1..3: constant schedule ----------------
+      // ---------------- chunks 1..4: constant schedule ----------------
+      // Chunk c's feed-forward (H += t) opens chunk c + 1's first asm group
+      // (8-byte adds at the pinned phase, sha256_dev.h rounds4_asm_ff).
+      St Hs{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+      St t = Hs;
+      const_chunk_lds<true>(t, lkw);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-        const_chunk_lds<true>(t, lkw + 64 * c);
-        H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
-        H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
-      }
+      for (int c = 1; c < 4; ++c) const_chunk_lds_ff(Hs, t, lkw + 64 * c);
       // ---------------- chunk 4 (last): only what the test needs ----------------
-      St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk_lds<true>(t, lkw + 64 * 3);
-      const uint32_t h0 = H[0] + t.a;
+      const uint32_t h0 = Hs.a + t.a;
 
       bool hit = h0 <= L.thr;
       if (FULL && hit) {
-        uint32_t D[8] = {h0, H[1] + t.b, H[2] + t.c, H[3] + t.d,
-                         H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
+        uint32_t D[8] = {h0, Hs.b + t.b, Hs.c + t.c, Hs.d + t.d,
+                         Hs.e + t.e, Hs.f + t.f, Hs.g + t.g, Hs.h + t.h};
         hit = full_test(D, L.diff);
       }
       if (MODE != 0) {
@@ -463,7 +479,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
           const unsigned long long rel = (unsigned long long)r * 62ull + j - L.off0;
           ok = rel < L.count;
           relv = (uint32_t)rel;
-          if (ok && rel < mymin) mymin = rel;
+          if (ok && relv < mymin) mymin = relv;
+          if (ok && relv == 0xFFFFFFFFu) atomicMin(&res->min_rel, rel);
         }
         const unsigned long long m = __ballot(ok);
         if (m) {  // wave-uniform
@@ -483,10 +500,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
     // wave min of the per-lane minima, one atomic per wave
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      const unsigned long long o = __shfl_xor(mymin, off, 64);
+      const uint32_t o = __shfl_xor(mymin, off, 64);
       mymin = o < mymin ? o : mymin;
     }
-    if (lane == 0 && mymin != ~0ull) atomicMin(&res->min_rel, mymin);
+    if (lane == 0 && mymin != 0xFFFFFFFFu) atomicMin(&res->min_rel, (unsigned long long)mymin);
   }
   if (MODE >= 1) {
     // The sentinel (workgroup 0, wave 0) is the only reader of host memory
@@ -551,7 +568,7 @@ template __global__ void pow_search<2, true>(const PowConsts*, PowLaunch, uint32
 // `res` reset themselves (the last wave to exit re-initialises them), and that
 // last wave also copies them to `hout`, mapped host memory: a launch is one
 // dispatch and no copy kernels.
-template <bool FULL, bool ANY>
+template <bool FULL, bool ANY, bool ASM>
 __global__ __launch_bounds__(256) void pow_search_lat(
     const PowConstsLat C0, PowLaunchLat L, PowResult* __restrict__ res, PowResult* __restrict__ hout) {
   (void)C0;
@@ -637,12 +654,12 @@ __global__ __launch_bounds__(256) void pow_search_lat(
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk_lds<false>(t, lk + 64 * c);
+      const_chunk_lds<ASM>(t, lk + 64 * c);
       H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
       H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
     }
     St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-    const_chunk_lds<false>(t, lk + 64 * 3);
+    const_chunk_lds<ASM>(t, lk + 64 * 3);
     // The whole digest stays live here (this kernel runs at <= 4 waves/SIMD,
     // so the 7 extra VGPRs cost no residency): a hit records it, and the
     // winner's block_hash needs no K2 launch (one serial SHA-256 of 5 chunks
@@ -707,10 +724,14 @@ __global__ __launch_bounds__(256) void pow_search_lat(
   }
 }
 
-template __global__ void pow_search_lat<false, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
-template __global__ void pow_search_lat<true, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
-template __global__ void pow_search_lat<false, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
-template __global__ void pow_search_lat<true, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, false, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, false, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, true, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, true, false>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, false, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, false, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<false, true, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
+template __global__ void pow_search_lat<true, true, true>(const PowConstsLat, PowLaunchLat, PowResult*, PowResult*);
 
 // K2: block_to_hash for n blocks; `msgs` holds each block's 270-byte message
 // already padded on the host to 320 bytes (80 big-endian words).
@@ -747,14 +768,23 @@ extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hi
   return hipGetLastError();
 }
 
-extern "C++" hipError_t pow_launch_search_lat(bool full, bool any, unsigned grid, hipStream_t stream,
-                                              const PowConstsLat& C, const PowLaunchLat& L, PowResult* res,
-                                              PowResult* hout) {
+extern "C++" hipError_t pow_launch_search_lat(bool full, bool any, bool asm_groups, unsigned grid,
+                                              hipStream_t stream, const PowConstsLat& C, const PowLaunchLat& L,
+                                              PowResult* res, PowResult* hout) {
   dim3 g(grid), b(256);
-  if (!full && !any) hipLaunchKernelGGL((pow_search_lat<false, false>), g, b, 0, stream, C, L, res, hout);
-  else if (!any) hipLaunchKernelGGL((pow_search_lat<true, false>), g, b, 0, stream, C, L, res, hout);
-  else if (!full) hipLaunchKernelGGL((pow_search_lat<false, true>), g, b, 0, stream, C, L, res, hout);
-  else hipLaunchKernelGGL((pow_search_lat<true, true>), g, b, 0, stream, C, L, res, hout);
+#define POW_LAT(F, A, G) hipLaunchKernelGGL((pow_search_lat<F, A, G>), g, b, 0, stream, C, L, res, hout)
+  if (asm_groups) {
+    if (!full && !any) POW_LAT(false, false, true);
+    else if (!any) POW_LAT(true, false, true);
+    else if (!full) POW_LAT(false, true, true);
+    else POW_LAT(true, true, true);
+  } else {
+    if (!full && !any) POW_LAT(false, false, false);
+    else if (!any) POW_LAT(true, false, false);
+    else if (!full) POW_LAT(false, true, false);
+    else POW_LAT(true, true, false);
+  }
+#undef POW_LAT
   return hipGetLastError();
 }
 

@@ -185,21 +185,6 @@ __device__ __forceinline__ St rounds4_kws_asm_from(const St& in, uint32_t k0, ui
                  [g] "v"(in.g), [h] "v"(in.h), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3));
   return St{o.e, o.f, o.g, o.h, o.a, o.b, o.c, o.d};
 }
-// Four chunk-0 rounds with uniform K (SGPR) and per-lane W.
-__device__ __forceinline__ void rounds4_ks_w_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
-                                                 uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
-  asm volatile(POW_PHASE
-               POW_R_KS_W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]", "%[w0]")
-               POW_R_KS_W("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]", "%[w1]")
-               POW_R_KS_W("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]", "%[w2]")
-               POW_R_KS_W("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]", "%[w3]")
-               : POW_STATE_OPS, POW_TEMPS
-               : [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3), [w0] "v"(w0), [w1] "v"(w1),
-                 [w2] "v"(w2), [w3] "v"(w3));
-  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
-}
-
 // A schedule word of chunk 0 (i >= 33): W = s1(W[i-2]) + W[i-7] + s0(W[i-15]) + W[i-16],
 // every instruction 8 bytes (v_lshrrev_b32_e64).  Uses t0..t3.
 #define POW_W(dst, wm2, wm7, wm15, wm16)                                \
@@ -237,6 +222,99 @@ __device__ __forceinline__ void rounds4_sched_asm(St& s, uint32_t k0, uint32_t k
   s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
 }
 
+// Chunk 0's schedule words 18-35 fold template-uniform and per-prefix terms
+// (DESIGN.md §4): their forms, every instruction 8 bytes, t0..t2 temporaries.
+//   POW_WA:  dst = x + y                       (y: VGPR or SGPR)
+//   POW_WS:  dst = s1(x) + y
+//   POW_WS3: dst = s1(x) + y + z
+#define POW_SIG1(x)                                                     \
+  "\tv_alignbit_b32 %[t0], " x ", " x ", 17\n"                        \
+  "\tv_alignbit_b32 %[t1], " x ", " x ", 19\n"                        \
+  "\tv_lshrrev_b32_e64 %[t2], 10, " x "\n"                            \
+  "\tv_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n"
+#define POW_WA(dst, x, y) "\tv_add_u32_e64 " dst ", " x ", " y "\n"
+#define POW_WS(dst, x, y) POW_SIG1(x) "\tv_add_u32_e64 " dst ", %[t0], " y "\n"
+#define POW_WS3(dst, x, y, z) POW_SIG1(x) "\tv_add3_u32 " dst ", %[t0], " y ", " z "\n"
+// The four round slots of a group: state names rotate by one per round.
+#define POW_R0(K, W) POW_R_KS_W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", K, W)
+#define POW_R1(K, W) POW_R_KS_W("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", K, W)
+#define POW_R2(K, W) POW_R_KS_W("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", K, W)
+#define POW_R3(K, W) POW_R_KS_W("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", K, W)
+#define POW_KS [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+
+// Chunk-0 rounds 16-35 in five groups G = 0..4 (rounds 16 + 4G .. 19 + 4G),
+// each schedule word computed inside the group just before its round.  w[] is
+// the chunk's schedule (w[16], w[17] given; the group writes its four words).
+// The uniform terms (SGPRs) and per-prefix terms (VGPRs):
+//   G = 0: ua = U18(j), ub = W3(j); pa = c18, pb = c19
+//   G = 1: ua, ub, uc = U20..U22;    pa = c23
+//   G = 2: ua, ub, uc = U25..U27;    pa = c24
+//   G = 3: ua, ub, uc = U28..U30;    pa = c31
+//   G = 4:                           pa = c32
+template <int G>
+__device__ __forceinline__ void rounds4_w_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t* w,
+                                              uint32_t ua, uint32_t ub, uint32_t uc, uint32_t pa, uint32_t pb) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  if constexpr (G == 0) {
+    (void)uc;
+    asm volatile(POW_PHASE
+                 POW_R0("%[k0]", "%[w16]") POW_R1("%[k1]", "%[w17]")
+                 POW_WA("%[w18]", "%[pa]", "%[ua]") POW_R2("%[k2]", "%[w18]")
+                 POW_WA("%[w19]", "%[pb]", "%[ub]") POW_R3("%[k3]", "%[w19]")
+                 : POW_STATE_OPS, POW_TEMPS, [w18] "=&v"(w[18]), [w19] "=&v"(w[19])
+                 : POW_KS, [w16] "v"(w[16]), [w17] "v"(w[17]), [pa] "v"(pa), [pb] "v"(pb), [ua] "s"(ua),
+                   [ub] "s"(ub));
+  } else if constexpr (G == 1) {
+    (void)pb;
+    asm volatile(POW_PHASE
+                 POW_WS("%[w20]", "%[w18]", "%[ua]") POW_R0("%[k0]", "%[w20]")
+                 POW_WS("%[w21]", "%[w19]", "%[ub]") POW_R1("%[k1]", "%[w21]")
+                 POW_WS("%[w22]", "%[w20]", "%[uc]") POW_R2("%[k2]", "%[w22]")
+                 POW_WS("%[w23]", "%[w21]", "%[pa]") POW_R3("%[k3]", "%[w23]")
+                 : POW_STATE_OPS, POW_TEMPS, [w20] "=&v"(w[20]), [w21] "=&v"(w[21]), [w22] "=&v"(w[22]),
+                   [w23] "=&v"(w[23])
+                 : POW_KS, [w18] "v"(w[18]), [w19] "v"(w[19]), [pa] "v"(pa), [ua] "s"(ua), [ub] "s"(ub),
+                   [uc] "s"(uc));
+  } else if constexpr (G == 2) {
+    (void)pb;
+    asm volatile(POW_PHASE
+                 POW_WS("%[w24]", "%[w22]", "%[pa]") POW_R0("%[k0]", "%[w24]")
+                 POW_WS3("%[w25]", "%[w23]", "%[w18]", "%[ua]") POW_R1("%[k1]", "%[w25]")
+                 POW_WS3("%[w26]", "%[w24]", "%[w19]", "%[ub]") POW_R2("%[k2]", "%[w26]")
+                 POW_WS3("%[w27]", "%[w25]", "%[w20]", "%[uc]") POW_R3("%[k3]", "%[w27]")
+                 : POW_STATE_OPS, POW_TEMPS, [w24] "=&v"(w[24]), [w25] "=&v"(w[25]), [w26] "=&v"(w[26]),
+                   [w27] "=&v"(w[27])
+                 : POW_KS, [w18] "v"(w[18]), [w19] "v"(w[19]), [w20] "v"(w[20]), [w22] "v"(w[22]),
+                   [w23] "v"(w[23]), [pa] "v"(pa), [ua] "s"(ua), [ub] "s"(ub), [uc] "s"(uc));
+  } else if constexpr (G == 3) {
+    (void)pb;
+    asm volatile(POW_PHASE
+                 POW_WS3("%[w28]", "%[w26]", "%[w21]", "%[ua]") POW_R0("%[k0]", "%[w28]")
+                 POW_WS3("%[w29]", "%[w27]", "%[w22]", "%[ub]") POW_R1("%[k1]", "%[w29]")
+                 POW_WS3("%[w30]", "%[w28]", "%[w23]", "%[uc]") POW_R2("%[k2]", "%[w30]")
+                 POW_WS3("%[w31]", "%[w29]", "%[w24]", "%[pa]") POW_R3("%[k3]", "%[w31]")
+                 : POW_STATE_OPS, POW_TEMPS, [w28] "=&v"(w[28]), [w29] "=&v"(w[29]), [w30] "=&v"(w[30]),
+                   [w31] "=&v"(w[31])
+                 : POW_KS, [w21] "v"(w[21]), [w22] "v"(w[22]), [w23] "v"(w[23]), [w24] "v"(w[24]),
+                   [w26] "v"(w[26]), [w27] "v"(w[27]), [pa] "v"(pa), [ua] "s"(ua), [ub] "s"(ub), [uc] "s"(uc));
+  } else {
+    // W33..35 are the generic form, into fresh registers: W17 is per prefix
+    // (live across the j-loop) and W18, W19 are read again by W34, W35
+    (void)ua, (void)ub, (void)uc, (void)pb;
+    asm volatile(POW_PHASE
+                 POW_WS3("%[w32]", "%[w30]", "%[w25]", "%[pa]") POW_R0("%[k0]", "%[w32]")
+                 POW_W("%[w33]", "%[w31]", "%[w26]", "%[w18]", "%[w17]") POW_R1("%[k1]", "%[w33]")
+                 POW_W("%[w34]", "%[w32]", "%[w27]", "%[w19]", "%[w18]") POW_R2("%[k2]", "%[w34]")
+                 POW_W("%[w35]", "%[w33]", "%[w28]", "%[w20]", "%[w19]") POW_R3("%[k3]", "%[w35]")
+                 : POW_STATE_OPS, POW_TEMPS, [w32] "=&v"(w[32]), [w33] "=&v"(w[33]), [w34] "=&v"(w[34]),
+                   [w35] "=&v"(w[35])
+                 : POW_KS, [w17] "v"(w[17]), [w18] "v"(w[18]), [w19] "v"(w[19]), [w20] "v"(w[20]),
+                   [w25] "v"(w[25]), [w26] "v"(w[26]), [w27] "v"(w[27]), [w28] "v"(w[28]), [w30] "v"(w[30]),
+                   [w31] "v"(w[31]), [pa] "v"(pa));
+  }
+  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
+}
+
 // In place: the state is read and written in the same registers.
 __device__ __forceinline__ void rounds4_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
@@ -269,6 +347,28 @@ __device__ __forceinline__ St rounds4_asm_from(const St& in, uint32_t k0, uint32
   return St{o.e, o.f, o.g, o.h, o.a, o.b, o.c, o.d};
 }
 
+
+// The previous chunk's feed-forward (H += t: 8 v_add_u32_e64) and the next
+// chunk's first four rounds from the new H, in one group: t (the previous
+// chunk's final state, dead once added) receives the new chunk's state, so
+// the group needs no registers beyond H, t and the temporaries.
+__device__ __forceinline__ void rounds4_asm_ff(St& H, St& t, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  asm volatile(POW_PHASE
+               "\tv_add_u32_e64 %[a], %[a], %[oa]\n\tv_add_u32_e64 %[b], %[b], %[ob]\n"
+               "\tv_add_u32_e64 %[c], %[c], %[oc]\n\tv_add_u32_e64 %[d], %[d], %[od]\n"
+               "\tv_add_u32_e64 %[e], %[e], %[oe]\n\tv_add_u32_e64 %[f], %[f], %[of]\n"
+               "\tv_add_u32_e64 %[g], %[g], %[og]\n\tv_add_u32_e64 %[h], %[h], %[oh]\n"
+               POW_RX("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[od]", "%[oh]", "%[k0]")
+               POW_RX("%[oh]", "%[a]", "%[b]", "%[c]", "%[od]", "%[e]", "%[f]", "%[g]", "%[oc]", "%[og]", "%[k1]")
+               POW_RX("%[og]", "%[oh]", "%[a]", "%[b]", "%[oc]", "%[od]", "%[e]", "%[f]", "%[ob]", "%[of]", "%[k2]")
+               POW_RX("%[of]", "%[og]", "%[oh]", "%[a]", "%[ob]", "%[oc]", "%[od]", "%[e]", "%[oa]", "%[oe]", "%[k3]")
+               : [oa] "+v"(t.a), [ob] "+v"(t.b), [oc] "+v"(t.c), [od] "+v"(t.d), [oe] "+v"(t.e), [of] "+v"(t.f),
+                 [og] "+v"(t.g), [oh] "+v"(t.h), [a] "+v"(H.a), [b] "+v"(H.b), [c] "+v"(H.c), [d] "+v"(H.d),
+                 [e] "+v"(H.e), [f] "+v"(H.f), [g] "+v"(H.g), [h] "+v"(H.h), POW_TEMPS
+               : [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
+  t = St{t.e, t.f, t.g, t.h, t.a, t.b, t.c, t.d};
+}
 
 // Generic compression of one chunk (used by the single-hash kernel K2; not on
 // the mining hot loop).  The schedule is a 16-word ring computed just ahead

@@ -228,3 +228,27 @@ def test_chunk_rounds_keep_one_phase(k1_code):
     eight = [x for x in chunk if x[2] == 8]
     off = [x for x in eight if x[0] % 8 != 4]
     assert len(eight) >= 3584 and len(off) <= 32, (len(eight), len(off))
+
+
+@pytest.mark.parametrize("variant", ["_Z10pow_searchILi0ELb0E", "_Z10pow_searchILi1ELb0E"])
+def test_trial_is_asm_groups(isa, variant):
+    """Every SHA-256 round and schedule word of the trial is in the asm groups
+    (8-byte encodings at the pinned phase); outside them the compiler emits
+    only the per-j set-up, the IV feed-forward of chunk 0 and the test:
+    <= 16 VALU instructions (round 2: ~135, with 4-byte encodings; a 4-byte
+    VOP2 op among 8-byte VOP3 ops issues at half rate, profiles/r03/probe/)."""
+    body = j_loop_body(isa, variant)
+    outside = re.sub(r";;#ASMSTART.*?;;#ASMEND", "", body, flags=re.S)
+    assert len(re.findall(r"^\s+v_", outside, flags=re.M)) <= 16
+
+
+@pytest.mark.parametrize("variant", ["_Z14pow_search_latILb0ELb0ELb1E", "_Z14pow_search_latILb0ELb1ELb1E"])
+def test_latency_kernel_asm_variant(isa, variant):
+    """K1' at 4 waves per SIMD runs chunks 1-4 as K1's asm groups: the
+    variant fits 4 waves per SIMD (<= 128 VGPRs) without scratch, and keeps
+    the 64 LDS reads inside the loop."""
+    md = metadata(isa, variant)
+    assert md["vgpr_count"] <= 128 and md["private_segment_fixed_size"] == 0 and md["vgpr_spill_count"] == 0, md
+    body = j_loop_body(isa, variant)
+    assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 64
+    assert body.count(".p2align 3") == 64
