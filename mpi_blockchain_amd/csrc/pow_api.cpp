@@ -348,8 +348,8 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // One dispatch: constants by value (kernarg), result published by the
   // kernel's last wave into mapped host memory (no copy kernels), `done` last.
   // At 4+ waves per SIMD (d = 20, 21) chunks 1-4 run as K1's asm groups
-  // (8-byte encodings at the pinned phase): time-to-block at d = 21 0.220 ->
-  // 0.212 ms.  At 1-2 waves per SIMD the kernel is latency-bound and the
+  // (8-byte encodings at the pinned phase): K1' at d = 21 7.79 -> 7.93 G
+  // trials/s, time-to-block 0.2136 -> 0.2125 ms (profiles/r03/ab/ab14_*).  At 1-2 waves per SIMD the kernel is latency-bound and the
   // compiler's interleaving of independent ops serves it better (d = 13:
   // 0.034 -> 0.038 ms with the groups; profiles/r03/ab/ab8_*).
   HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, ctx->stream,
