@@ -459,17 +459,19 @@ TRIAL_FULL_RATE = 2065
 
 
 def valu_peaks(miner, device: int, cu_count: int) -> dict:
-    """Measured ceilings (pow_valu_rate, include/pow_tools.h): the full-rate
-    chain (v_bitop3_b32 + v_add_u32, the SIMD-32 ceiling), the half-rate chain
-    (v_alignbit_b32 + v_add3_u32), the SHA mix, each with the clock the chip
-    held; and the mix-adjusted ceiling: K1's trial mix (TRIAL_*_RATE) issued at
-    the two isolated rates, priced at 5,000 algorithmic ops per hash."""
+    """Measured ceilings (pow_valu_rate, include/pow_tools.h; every stream 8-byte
+    encodings at K1's code phase): the full-rate chain (v_bitop3_b32 +
+    v_add_u32_e64, the SIMD-32 ceiling), the half-rate chain (v_alignbit_b32 +
+    v_add3_u32), and K1's SHA-256 round stream alone (no schedule words), each
+    with the clock the chip held; and the mix-adjusted ceiling: K1's trial mix
+    (TRIAL_*_RATE) issued at the two isolated rates, priced at 5,000
+    algorithmic ops per hash."""
     import ctypes
 
     from mpi_blockchain_amd._lib import POW_VALU_FULL, POW_VALU_HALF, POW_VALU_MIX, ValuResult
 
     out = {}
-    for name, kind in (("full_rate", POW_VALU_FULL), ("half_rate", POW_VALU_HALF), ("sha_mix", POW_VALU_MIX)):
+    for name, kind in (("full_rate", POW_VALU_FULL), ("half_rate", POW_VALU_HALF), ("sha_round", POW_VALU_MIX)):
         r = ValuResult()
         if miner.L.pow_valu_rate(device, kind, ctypes.byref(r)) == 0:
             out[f"microbench_{name}"] = {"tops": round(r.lane_ops_per_s / 1e12, 2),

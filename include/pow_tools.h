@@ -10,8 +10,8 @@ extern "C" {
 
 /* Instruction mixes of pow_valu_rate. */
 enum {
-  POW_VALU_MIX = 0,  /* v_alignbit_b32 + v_bitop3_b32 + v_add3_u32: the SHA-256 kinds (2 half : 1 full rate) */
-  POW_VALU_FULL = 1, /* v_bitop3_b32 + v_add_u32, VGPR operands: full rate (the SIMD-32 ceiling) */
+  POW_VALU_MIX = 0,  /* K1's SHA-256 round stream (6 alignbit, 4 bitop3, 2 add3, 2 add: 8 half : 6 full rate) */
+  POW_VALU_FULL = 1, /* v_bitop3_b32 + v_add_u32_e64, VGPR operands: full rate (the SIMD-32 ceiling) */
   POW_VALU_HALF = 2, /* v_alignbit_b32 + v_add3_u32: half rate */
 };
 

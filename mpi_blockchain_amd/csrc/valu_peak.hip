@@ -1,16 +1,19 @@
 // Int32 VALU issue-rate microbenchmarks for the roofline (include/pow_tools.h).
 //
-// Every CU runs 8 waves per SIMD of 8 independent dependency chains per lane,
-// one of three instruction mixes:
-//   POW_VALU_MIX   v_alignbit_b32 + v_bitop3_b32 + v_add3_u32 per step: the
-//                  three instruction kinds that make up ~97% of the SHA-256
-//                  kernel (2 half-rate : 1 full-rate on gfx950);
-//   POW_VALU_FULL  v_bitop3_b32 + v_add_u32, VGPR operands only: the full-rate
-//                  ceiling (SIMD-32: one wave64 instruction per 2 cycles);
-//   POW_VALU_HALF  v_alignbit_b32 + v_add3_u32: the half-rate kinds alone.
-// Each workgroup also stamps the shader clock (s_memtime) against the
-// constant-rate realtime counter (s_memrealtime), so the clock the chip held
-// during the run is measured, not assumed.
+// Every CU runs 8 waves per SIMD; each loop iteration is one asm block of
+// 8-byte VALU instructions held 4 bytes past an 8-byte boundary (the phase
+// K1's trial runs at), one of three streams:
+//   POW_VALU_MIX   K1's SHA-256 round as it issues it (sha256_dev.h POW_R):
+//                  8 rounds, 6 v_alignbit_b32 + 4 v_bitop3_b32 + 2 v_add3_u32
+//                  + 2 v_add_u32_e64 each (8 half-rate : 6 full-rate);
+//   POW_VALU_FULL  v_bitop3_b32 + v_add_u32_e64 over 8 independent chains,
+//                  VGPR operands only: the full-rate ceiling (SIMD-32: one
+//                  wave64 instruction per 2 cycles);
+//   POW_VALU_HALF  v_alignbit_b32 + v_add3_u32 over 8 chains: half rate.
+// Pure streams cost the same at either code phase; mixed ones do not
+// (profiles/r03/probe/).  Each workgroup also stamps the shader clock
+// (s_memtime) against the constant-rate realtime counter (s_memrealtime), so
+// the clock the chip held during the run is measured, not assumed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,8 +22,14 @@
 
 #include "../../include/pow_gpu.h"
 #include "../../include/pow_tools.h"
+#include "sha256_dev.h"
 
-#define VP_ITERS 4096
+#define VP_ITERS 2048
+
+// one chain step: FULL x = bitop3(x, y, z) + y; HALF x = rotr(x, 7) + x + y
+#define VP_F(x) "\tv_bitop3_b32 " x ", " x ", %[y], %[z] bitop3:0x96\n\tv_add_u32_e64 " x ", " x ", %[y]\n"
+#define VP_H(x) "\tv_alignbit_b32 %[r], " x ", " x ", 7\n\tv_add3_u32 " x ", %[r], " x ", %[y]\n"
+#define VP_CHAINS(M) M("%[x0]") M("%[x1]") M("%[x2]") M("%[x3]") M("%[x4]") M("%[x5]") M("%[x6]") M("%[x7]")
 
 template <int KIND>
 __global__ __launch_bounds__(256) void valu_rate_kernel(uint32_t seed, uint32_t* out, unsigned long long* stamps) {
@@ -33,21 +42,34 @@ __global__ __launch_bounds__(256) void valu_rate_kernel(uint32_t seed, uint32_t*
 #pragma unroll
   for (int k = 0; k < 8; ++k) x[k] = seed + (uint32_t)k * 0x9e3779b9u + threadIdx.x;
   for (int it = 0; it < VP_ITERS; ++it) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (KIND == POW_VALU_MIX) {
-        const uint32_t r = __builtin_amdgcn_alignbit(x[k], x[k], 7 + k);
-        const uint32_t b = __builtin_amdgcn_bitop3_b32(r, y, z, 0x96);
-        x[k] = b + x[k] + r;  // v_add3_u32
-      } else if (KIND == POW_VALU_FULL) {
-        // v_bitop3_b32 then v_add_u32 ((x ^ y) + z would fuse into v_xad_u32, half rate)
-        x[k] = __builtin_amdgcn_bitop3_b32(x[k], y, z, 0x96) + y;
-      } else {
-        const uint32_t r = __builtin_amdgcn_alignbit(x[k], x[k], 7 + k);
-        x[k] = r + x[k] + y;  // v_add3_u32
-      }
+    if (KIND == POW_VALU_MIX) {
+      powdev::St s{x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]};
+      uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+      // 8 rounds: the state's names rotate by one per round, back to the start
+      asm volatile(POW_PHASE
+                   POW_R("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[y]")
+                   POW_R("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[y]")
+                   POW_R("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[y]")
+                   POW_R("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[y]")
+                   POW_R("%[e]", "%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[y]")
+                   POW_R("%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[y]")
+                   POW_R("%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[y]")
+                   POW_R("%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[a]", "%[y]")
+                   : POW_STATE_OPS, POW_TEMPS
+                   : [y] "v"(y));
+      x[0] = s.a; x[1] = s.b; x[2] = s.c; x[3] = s.d; x[4] = s.e; x[5] = s.f; x[6] = s.g; x[7] = s.h;
+    } else if (KIND == POW_VALU_FULL) {
+      asm volatile(POW_PHASE VP_CHAINS(VP_F)
+                   : [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [x4] "+v"(x[4]),
+                     [x5] "+v"(x[5]), [x6] "+v"(x[6]), [x7] "+v"(x[7])
+                   : [y] "v"(y), [z] "v"(z));
+    } else {
+      uint32_t rr;
+      asm volatile(POW_PHASE VP_CHAINS(VP_H)
+                   : [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [x4] "+v"(x[4]),
+                     [x5] "+v"(x[5]), [x6] "+v"(x[6]), [x7] "+v"(x[7]), [r] "=&v"(rr)
+                   : [y] "v"(y));
     }
-    asm volatile("" : "+v"(y), "+v"(z));
   }
   uint32_t acc = 0;
 #pragma unroll
@@ -59,9 +81,9 @@ __global__ __launch_bounds__(256) void valu_rate_kernel(uint32_t seed, uint32_t*
   }
 }
 
-// VALU wave-instructions per lane-step of each kind (the loop's counter and
-// branch are scalar): checked against the disassembly in tests/test_build.py.
-static int instrs_per_step(int kind) { return kind == POW_VALU_MIX ? 3 : 2; }
+// VALU wave-instructions per loop iteration of each kind (the loop's counter
+// and branch are scalar): checked against the disassembly in tests/test_build.py.
+static int instrs_per_iter(int kind) { return kind == POW_VALU_MIX ? 8 * 14 : 16; }
 
 extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   if (!res || kind < POW_VALU_MIX || kind > POW_VALU_HALF) return POW_EINVAL;
@@ -117,7 +139,7 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   (void)hipFree(out);
   (void)hipFree(stamps);
   if (rc != POW_OK) return rc;
-  const double wave_instr = (double)grid * 4.0 * VP_ITERS * 8.0 * instrs_per_step(kind);
+  const double wave_instr = (double)grid * 4.0 * VP_ITERS * instrs_per_iter(kind);
   res->lane_ops_per_s = wave_instr * 64.0 / (best * 1e-3);
   res->kernel_ms = best;
   res->clock_hz = best_clock;

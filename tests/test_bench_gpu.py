@@ -45,8 +45,8 @@ def test_bench_json_contract():
 
 def test_valu_microbench_ceilings():
     """pow_valu_rate: the full-rate chain issues faster than the half-rate one
-    (about 2x), each at a measured clock; the mix-adjusted ceiling lies
-    between them."""
+    (about 2x), each at a measured clock; K1's SHA round stream lies between
+    them."""
     import ctypes
 
     sys.path.insert(0, ROOT)
@@ -62,6 +62,9 @@ def test_valu_microbench_ceilings():
         out[k] = r
     assert 1.5 < out[POW_VALU_FULL].lane_ops_per_s / out[POW_VALU_HALF].lane_ops_per_s < 2.5
     assert 1.9 < out[POW_VALU_FULL].cycles_per_instr < 2.6 and 3.6 < out[POW_VALU_HALF].cycles_per_instr < 4.6
+    # K1's round stream (8 half : 6 full rate) lies between the two (~3.66 in the probes)
+    assert out[POW_VALU_FULL].cycles_per_instr < out[POW_VALU_MIX].cycles_per_instr < \
+        out[POW_VALU_HALF].cycles_per_instr
     assert L.pow_valu_rate(0, 7, ctypes.byref(ValuResult())) < 0
 
 
