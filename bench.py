@@ -512,6 +512,15 @@ def roofline_block(achieved, kms, peak, live, traffic, traffic_source, algo_byte
             # VALU lane-ops the counters saw issued, over the same kernel's duration in the pass
             r["issued_frac_at_measured_clock"] = round(
                 v["counters"]["SQ_INSTS_VALU"] * 64 / (v["kernel_ns"] * 1e-9) / 1e12 / peak_clk, 4)
+            # Issue efficiency, clock-free: K1's trial mix priced at the isolated
+            # per-instruction cycles of the two microbenchmark streams, over the
+            # cycles per VALU instruction the counters measured (1.0 = no mixing cost)
+            f, h = peak.get("microbench_full_rate"), peak.get("microbench_half_rate")
+            if f and h and v.get("cycles_per_valu_instr"):
+                iso = ((TRIAL_HALF_RATE * h["cycles_per_instr"] + TRIAL_FULL_RATE * f["cycles_per_instr"])
+                       / (TRIAL_HALF_RATE + TRIAL_FULL_RATE))
+                r["isolated_rate_cycles_per_instr"] = round(iso, 3)
+                r["issue_efficiency_vs_isolated_rates"] = round(iso / v["cycles_per_valu_instr"], 4)
     return r
 
 

@@ -119,6 +119,13 @@ def test_live_valu_counters(monkeypatch):
     assert r["valu_instr_per_hash"] == v["valu_instr_per_hash"]
     assert abs(r["frac_at_measured_clock"] - 43.28 / (1024 * 32 * clk / 1e12)) < 1e-4
     assert 0 < r["issued_frac_at_measured_clock"] < r["frac_at_measured_clock"]
+    # with the microbenchmark cycles: K1's mix at the isolated rates over the measured cycles
+    peak = {"nominal_tops": 78.64, "microbench_full_rate": {"cycles_per_instr": 2.2},
+            "microbench_half_rate": {"cycles_per_instr": 4.2}}
+    r = bench.roofline_block(43.28, 496.2, peak, {"valu": v}, 1, "x", 1, 256)
+    iso = (bench.TRIAL_HALF_RATE * 4.2 + bench.TRIAL_FULL_RATE * 2.2) / (bench.TRIAL_HALF_RATE + bench.TRIAL_FULL_RATE)
+    assert abs(r["isolated_rate_cycles_per_instr"] - iso) < 1e-3
+    assert abs(r["issue_efficiency_vs_isolated_rates"] - iso / v["cycles_per_valu_instr"]) < 1e-3
 
 
 def test_mix_adjusted_ceiling_math():
