@@ -6,7 +6,8 @@
 //     leading-zero-bit test (block.cpp:91-96, trap T3) for every counter of a
 //     range.  MODE 0 = sweep (record every solution), 1 = mine (lowest
 //     solving counter, early exit).  FULL = difficulty > 32 bits.
-// K2  pow_hash_kernel — block_to_hash (block.cpp:74-77) for a batch of blocks.
+// K2  pow_hash_kernel — block_to_hash (block.cpp:74-77) for a batch of blocks;
+// K2' pow_hash_one — the same for ONE block at low latency (validation).
 //
 // Work decomposition of K1 (DESIGN.md "Kernel K1"): counter c = 62*P + j.
 //   * one LANE owns a prefix P (nonce chars 0..7, message words W1, W2);
@@ -754,6 +755,62 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
   for (int k = 0; k < 8; ++k) digests[(size_t)i * 8u + k] = h[k];
 }
 
+// K2': block_to_hash (block.cpp:74-77) of ONE block, for validation
+// (pow_hash_block).  A received block is checked one at a time
+// (validate_block_for_chain, node.cpp:199-253), so the latency of one hash is
+// what counts: one wave, the message by value in the kernarg segment (no H2D
+// copy), the digest and a done word stored into mapped host memory (no D2H
+// copy, no completion-signal wait).  The five chunks' message schedules do not
+// depend on the chaining state, so lanes 0-4 expand them at once (one chunk
+// each, K folded in: K+W into LDS); every lane then runs the 320 rounds
+// (the same values in every lane: no divergence) reading K+W from LDS 4 at a
+// time, and lane 0 publishes.  <= 64 VGPRs: it must fit the workgroup slot a
+// running K1 leaves free.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void pow_hash_one(
+    const PowMsg M, PowHashOut* __restrict__ hout, uint32_t seq) {
+  (void)M;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  // M is the first kernel argument: read it through the kernarg pointer (its
+  // address would make a private copy).  Lane c < 5 reads its chunk's 16 words.
+  const uint32_t* const msg = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  __shared__ __attribute__((aligned(16))) uint32_t kw[5][64];
+  const uint32_t lane = threadIdx.x;
+  if (lane < 5u) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = msg[16u * lane + k];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      if (i >= 16) w[i & 15] = ssig1(w[(i + 14) & 15]) + w[(i + 9) & 15] + ssig0(w[(i + 1) & 15]) + w[i & 15];
+      kw[lane][i] = K[i] + w[i & 15];
+    }
+  }
+  __syncthreads();
+  St h{IV[0], IV[1], IV[2], IV[3], IV[4], IV[5], IV[6], IV[7]};
+#pragma unroll 1
+  for (int c = 0; c < 5; ++c) {
+    St t = h;
+#pragma unroll
+    for (int g = 0; g < 64; g += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&kw[c][g]);
+      round_k_w(t, v.x, 0u);
+      round_k_w(t, v.y, 0u);
+      round_k_w(t, v.z, 0u);
+      round_k_w(t, v.w, 0u);
+    }
+    h.a += t.a; h.b += t.b; h.c += t.c; h.d += t.d;
+    h.e += t.e; h.f += t.f; h.g += t.g; h.h += t.h;
+  }
+  if (lane == 0) {
+    const uint32_t d[8] = {h.a, h.b, h.c, h.d, h.e, h.f, h.g, h.h};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __hip_atomic_store(&hout->digest[k], d[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hout->ticks, __builtin_amdgcn_s_memrealtime() - t0, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hout->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ---- host-side launch wrappers (called from pow_api.cpp) ----
 extern "C++" hipError_t pow_launch_search(int mode, bool full, unsigned grid, hipStream_t stream,
                                           const PowConsts* C, const PowLaunch& L, uint32_t* out,
@@ -785,6 +842,11 @@ extern "C++" hipError_t pow_launch_search_lat(bool full, bool any, bool asm_grou
     else POW_LAT(true, true, false);
   }
 #undef POW_LAT
+  return hipGetLastError();
+}
+
+extern "C++" hipError_t pow_launch_hash_one(hipStream_t stream, const PowMsg& M, PowHashOut* hout, uint32_t seq) {
+  hipLaunchKernelGGL(pow_hash_one, dim3(1), dim3(64), 0, stream, M, hout, seq);
   return hipGetLastError();
 }
 

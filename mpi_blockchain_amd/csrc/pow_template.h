@@ -147,6 +147,21 @@ struct PowResult {
   PowHit hit[POW_HITS];
 };
 
+// K2' (pow_hash_block's one-block path): the padded 320-byte message as 80
+// big-endian words, passed by value (kernarg: no H2D copy) ...
+struct PowMsg {
+  uint32_t w[80];
+};
+// ... and its result, written by the kernel into mapped host memory (no D2H
+// copy): the digest, the kernel's duration in realtime ticks, and `done` = the
+// launch's seq, stored last (system scope) for the host to poll.
+struct PowHashOut {
+  uint32_t digest[8];
+  unsigned long long ticks;
+  unsigned int done;
+  unsigned int pad;
+};
+
 // Constants and result words of a context, contiguous so that one H2D copy
 // from a pinned staging twin refreshes both before a launch.
 struct PowBlob {

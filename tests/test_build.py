@@ -105,6 +105,15 @@ def test_k2_fits_beside_k1(isa):
     assert md["vgpr_spill_count"] == 0 and md["private_segment_fixed_size"] == 0, md
 
 
+def test_k2_one_block_fits_beside_k1(isa):
+    """K2' (pow_hash_block's one-block path) runs in the same free workgroup
+    slot as K2: <= 64 VGPRs, no scratch (its by-value message is read through
+    the kernarg pointer, not copied), LDS only for the five K+W schedules."""
+    md = metadata(isa, "_Z12pow_hash_one")
+    assert md["vgpr_count"] <= 64, md
+    assert md["vgpr_spill_count"] == 0 and md["private_segment_fixed_size"] == 0, md
+
+
 @pytest.mark.parametrize("variant", ["_Z14pow_search_latILb0ELb0E", "_Z14pow_search_latILb0ELb1E"])
 def test_latency_kernel_no_private_copy(isa, variant):
     """The latency kernel reads its by-value constants through the kernarg

@@ -84,6 +84,30 @@ def test_random_block_digests(miner, golden):
     assert miner.digest(b).hex() == golden["random_blocks"][0]["hex"]
 
 
+def test_single_block_path(miner, golden, templates):
+    """pow_hash_block (one block: K2', message by value, digest into mapped
+    host memory) on every golden random block and edge-counter digest, one
+    call each, against the reference's digests; and its call latency."""
+    import statistics
+    import time
+
+    for e in golden["random_blocks"]:
+        assert miner.block_to_hash(block_from_random(e)) == e["hex"]
+    for e in golden["digests"]:
+        b = with_nonce(block_from_template(templates[e["template"]]), nonce_from_counter(e["counter"]))
+        assert miner.block_to_hash(b) == e["hex"]
+    b = block_from_random(golden["random_blocks"][0])
+    lat = []
+    for _ in range(50):
+        t = time.perf_counter()
+        miner.block_to_hash(b)
+        lat.append(time.perf_counter() - t)
+    st = miner.stats()
+    assert st["launches"] == 1 and st["hashes"] == 1 and 0 < st["kernel_ms"] < 1.0, st
+    print(f"pow_hash_block: call median {statistics.median(lat) * 1e6:.1f} us, kernel {st['kernel_ms'] * 1e3:.1f} us")
+    assert statistics.median(lat) < 0.001, lat
+
+
 def test_messages(golden, templates):
     for name, hx in golden["messages"].items():
         b = with_nonce(block_from_template(templates[name]), nonce_from_counter(0))
