@@ -116,7 +116,7 @@ __device__ __forceinline__ void const_chunk_lds_ff(St& H, St& t, const uint32_t*
   POW_SB();
 }
 
-// Append the 32-entry-aligned part of a wave's staged solutions (nst <= 127,
+// Append the 32-entry-aligned part of a wave's staged solutions (nst <= 255,
 // in LDS) to the global list with one atomic; the remainder (< 32) moves to
 // the stage front.  Every reservation is a multiple of 32 entries, so each
 // block starts on a 128-byte line of `out` (hipMalloc alignment) and lanes
@@ -129,7 +129,7 @@ __device__ __forceinline__ void flush_stage(uint32_t* wst, uint32_t& nst, uint32
   unsigned long long got = 0;
   if (lane == 0) got = atomicAdd(&res->count, (unsigned long long)n);
   const unsigned long long base = uniform64(got);  // 64-bit: 2^32 solutions at d = 0
-  const uint32_t i = lane * 4u;  // n <= 96: one pass of <= 24 lanes
+  const uint32_t i = lane * 4u;  // n <= 224: one pass of <= 56 lanes
   if (i < n) {
     const uint32_t e0 = wst[i], e1 = wst[i + 1u], e2 = wst[i + 2u], e3 = wst[i + 3u];
     const unsigned long long o = base + i;
@@ -250,11 +250,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t iters = 0;
   // Sweep mode: solutions are staged per wave in LDS and flushed in 32-entry
-  // blocks (one atomic + whole-line stores per >= 64 solutions); the lowest solution
+  // blocks (one atomic + whole-line stores per >= 192 solutions); the lowest solution
   // is kept per lane and min-reduced once per wave at exit.  One atomic per
   // solution would make every solution a separate memory-side request
-  // (~0.68 GB of requests per 2^32 sweep at d = 9 for 34 MB of data).
-  __shared__ __attribute__((aligned(16))) uint32_t stage[4][128];
+  // (~0.68 GB of requests per 2^32 sweep at d = 9 for 34 MB of data).  A
+  // 256-entry stage flushed at >= 192 (round 3; was 128 at >= 64) cut the
+  // flush atomics ~3x: WRITE_SIZE 42.8 -> 40.0 MB per 2^32 window at equal
+  // speed (profiles/r03/ab/ab16_*).
+  __shared__ __attribute__((aligned(16))) uint32_t stage[4][256];
   uint32_t* wst = stage[threadIdx.x >> 6];
   uint32_t nst = 0;                     // staged entries (wave-uniform)
   // lowest solution of this lane, 32-bit (a sweep window is <= 2^32 counters,
@@ -489,7 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
           if (ok) wst[nst + rank] = relv;
           nst += (uint32_t)__popcll(m);
-          if (nst >= 64) flush_stage(wst, nst, lane, res, out, L.cap);
+          if (nst >= 192) flush_stage(wst, nst, lane, res, out, L.cap);
         }
       }
     }

@@ -24,7 +24,8 @@
 #include "../../include/pow_tools.h"
 #include "sha256_dev.h"
 
-#define VP_ITERS 2048
+// iterations: ~2-3 ms per stream, long enough for a steady clock reading
+#define VP_ITERS(kind) ((kind) == POW_VALU_MIX ? 2048 : 16384)
 
 // one chain step: FULL x = bitop3(x, y, z) + y; HALF x = rotr(x, 7) + x + y
 #define VP_F(x) "\tv_bitop3_b32 " x ", " x ", %[y], %[z] bitop3:0x96\n\tv_add_u32_e64 " x ", " x ", %[y]\n"
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void valu_rate_kernel(uint32_t seed, uint32_t*
   uint32_t x[8], y = seed ^ threadIdx.x, z = seed * 3u + blockIdx.x;
 #pragma unroll
   for (int k = 0; k < 8; ++k) x[k] = seed + (uint32_t)k * 0x9e3779b9u + threadIdx.x;
-  for (int it = 0; it < VP_ITERS; ++it) {
+  for (int it = 0; it < VP_ITERS(KIND); ++it) {
     if (KIND == POW_VALU_MIX) {
       powdev::St s{x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]};
       uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
@@ -139,7 +140,7 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   (void)hipFree(out);
   (void)hipFree(stamps);
   if (rc != POW_OK) return rc;
-  const double wave_instr = (double)grid * 4.0 * VP_ITERS * instrs_per_iter(kind);
+  const double wave_instr = (double)grid * 4.0 * VP_ITERS(kind) * instrs_per_iter(kind);
   res->lane_ops_per_s = wave_instr * 64.0 / (best * 1e-3);
   res->kernel_ms = best;
   res->clock_hz = best_clock;
