@@ -33,7 +33,8 @@ build)
     -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/mine_chain"
   $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g $SAN -pthread -I "$R/include" "$R/examples/board_two_ctx.c" \
     -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/board_two_ctx"
-  $CLANGXX -std=c++17 -O1 -g $SAN -pthread -I "$R/include" -I "$MPI_INC" \
+  # the test build of the node (-DPOW_NODE_TEST_KNOBS): the runs below use its race-shaping switches
+  $CLANGXX -std=c++17 -O1 -g $SAN -pthread -DPOW_NODE_TEST_KNOBS -I "$R/include" -I "$MPI_INC" \
     "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' \
     "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$O/pow_node"
   echo "built $O"
@@ -60,6 +61,11 @@ run)
   echo "chains d=5:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   echo "protocol paths taken (lost races, branch conflicts, chain requests):"
   grep -c "Perdí la carrera\|Conflicto\|TAG_CHAIN_HASH" net_d5.log || true
+  rm -f ./*.out
+  # the mutual chain-request case (round 3): every rank 3 blocks ahead on a private branch
+  /opt/conda/bin/mpiexec -np 2 "$O/pow_node" --difficulty 9 --serial-init 1 --private-lead 3 > net_mutual.log
+  cat net_mutual.log
+  echo "chains (mutual requests):"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   ;;
 tsan-build)
   # ThreadSanitizer on pow_node's own code (receive thread, miner thread, GPU
@@ -73,7 +79,7 @@ tsan-build)
     -Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer -I "$R/include" -I "$C" \
     "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
     "$C/valu_peak.hip" -o "$T/libpow_gpu.so"
-  $CLANGXX -std=c++17 -O1 -g -fsanitize=thread -pthread -I "$R/include" -I "$MPI_INC" \
+  $CLANGXX -std=c++17 -O1 -g -fsanitize=thread -pthread -DPOW_NODE_TEST_KNOBS -I "$R/include" -I "$MPI_INC" \
     "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$T" -lpow_gpu \
     -Wl,-rpath,'$ORIGIN' "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$T/pow_node_tsan"
   $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g -fsanitize=thread -pthread -I "$R/include" \
@@ -100,6 +106,10 @@ tsan-run)
   echo "chains d=5:"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   echo "protocol paths taken (lost races, branch conflicts, chain requests):"
   grep -c "Perdí la carrera\|Conflicto\|TAG_CHAIN_HASH" net_d5.log || true
+  rm -f ./*.out
+  /opt/conda/bin/mpiexec -np 2 "$T/pow_node_tsan" --difficulty 9 --private-lead 3 > net_mutual.log
+  cat net_mutual.log
+  echo "chains (mutual requests):"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   ;;
 *)
   echo "usage: $0 build|run|tsan-build|tsan-run" >&2; exit 2;;
