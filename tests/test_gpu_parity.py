@@ -339,6 +339,32 @@ def test_full_window_2p32(miner, fingerprints, templates):
         assert mn == lad[d]["first"][0]
 
 
+@pytest.mark.parametrize("nranks", [3, 8])
+def test_shard_union_equals_full_window(miner, fingerprints, templates, nranks):
+    """SURVEY.md §4 item 4 at full size: the static shards of [0, 2^32)
+    (pow_group_partition, unaligned for 3 ranks), each swept on its own as a
+    rank of config 4 would, unite to exactly the single window's solution set
+    (count + sha256 of the sorted list = the CPU fingerprints), and the lowest
+    counter over the shards is the window's first solution."""
+    import numpy as np
+
+    from mpi_blockchain_amd.shard import native_partition
+
+    b = block_from_template(templates["S0"])
+    parts, lows = [], []
+    for r in range(nranks):
+        s, k = native_partition(0, 1 << 32, r, nranks)
+        got = miner.sweep(b, s, k, 9, cap=9_000_000 // nranks + 100_000)
+        parts.append(got.astype(np.uint64) + s)
+        if got.size:
+            lows.append(int(got[0]) + s)
+    union = np.sort(np.concatenate(parts)).astype(np.uint32)
+    lad = fingerprints["ladder"]["9"]
+    assert union.size == lad["count"]
+    assert fp(union) == lad["sha256_le_u32"]
+    assert min(lows) == lad["first"][0]
+
+
 @pytest.mark.parametrize("name", ["S1", "S2"])
 def test_full_window_2p32_S1(miner, templates, name):
     """Config 2 at full size on the other golden templates:
