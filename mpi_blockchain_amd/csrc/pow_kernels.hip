@@ -395,9 +395,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       // 2^32 window).  The alignment pins that phase whatever code precedes the
       // loop; it costs at most one s_nop per trial (tests/test_build.py).
       asm volatile(".p2align 3");
-      // Every round in round_ordered's issue order (sha256_dev.h); each
-      // schedule word is computed just before its round (computing it one
-      // round earlier measured 0.9% slower, profiles/r02/ab/ab8).
+      // Every round and schedule word of the trial is hand-written asm, four
+      // rounds per group, each group at the pinned code phase (sha256_dev.h;
+      // DESIGN.md §4 "Code placement"), the rounds in round_ordered's issue
+      // order; each schedule word is computed just before its round
+      // (computing it one round earlier measured 0.9% slower, profiles/r02/ab/ab8).
       POW_SB();
       St s = rounds4_kws_asm_from(s4, J[PC_KW0 + 4], J[PC_KW0 + 5], J[PC_KW0 + 6], J[PC_KW0 + 7]);
 #pragma unroll
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
           w[i + 3] = q[3];
           return;
         }
-        // rounds 16-35: the folded schedule words (wcalc's forms) inside the groups
+        // rounds 16-35: the folded schedule words inside the groups
         POW_SB();
         if (i == 16)
           rounds4_w_asm<0>(s, Kx[16], Kx[17], Kx[18], Kx[19], w, J[PC_U18 + j], J[PC_W3 + j], 0u, c18, c19);
