@@ -6,6 +6,7 @@ Run on an MI355X:  python -m pytest tests -m gpu -x -q
 """
 import hashlib
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -456,6 +457,21 @@ def test_random_templates_vs_oracle(miner):
         got = miner.sweep(make_block(idx, own, dif, cat, prev), start, count, d)
         want, n = O.sweep(make_oblock(idx, own, dif, cat, prev), start, count, d, cap=count, threads=threads)
         assert got.tolist() == want.tolist(), (k, start, count, d)
+
+
+def test_parity_fuzz():
+    """Randomised parity (tests/parity_fuzz.py): 120 random templates, window
+    starts (anywhere, straddling 2^32 multiples and base-62 carries, the end
+    of the counter space), lengths and difficulties 0..14: pow_sweep's list ==
+    the oracle's, pow_mine == its first, pow_mine_any in it, and the winner's
+    digest == the oracle's, the reference's (oracle/_ref) and K2''s."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import parity_fuzz
+
+    with GpuMiner(0) as m:
+        res = parity_fuzz.run(120, 2024, miner=m)
+    assert res.get("ok"), res
+    assert res["cases"] == 120 and res["solutions"] > 0
 
 
 def test_sweep_d0_full_window_count():
