@@ -92,7 +92,13 @@ __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { rou
 
 // Four rounds of a constant-schedule chunk (K+W from LDS) as ONE asm block:
 // 56 VALU instructions, every one 8 bytes long (v_add_u32_e64, never the
-// 4-byte VOP2 form hipcc picks), in the order hipcc emitted round_ordered.
+// 4-byte VOP2 form hipcc picks).  Each round issues the e-path first, its
+// full-rate ops between the rotations (rotr e 6, Ch, Maj, rotr e 11, h + K+W,
+// rotr e 25, S1, T1, e'), then the a-path (three rotations, S0, a'):
+// 0.22-0.31% less kernel time than round_ordered's order (Ch, Maj, the six
+// rotations, S0, S1, then the adds) in three A/B runs at the pinned phase
+// (profiles/r03/ab/ab17_*); every form measured within 2% in isolation
+// (tools/round_probe.hip).
 // Each block starts with `.p2align 3; s_nop 0`, so every VALU instruction of
 // a chunk sits 4 bytes past an 8-byte boundary whatever the compiler puts
 // before the block (its s_waitcnt for the LDS words, a hazard s_nop): on
@@ -101,19 +107,19 @@ __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { rou
 //   POW_RX(a, b, c, d, e, f, g, h, d', h', KW): one round reading a..h and
 //   writing e' into d' and a' into h' (d' = d, h' = h for in-place).
 #define POW_RX(a, b, c, d, e, f, g, h, dd, hh, KW)                     \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                           \
   "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"             \
   "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"             \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                          \
+  "\tv_add_u32_e64 " hh ", " h ", " KW "\n"                             \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                          \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"             \
+  "\tv_add3_u32 " hh ", " hh ", %[t5], %[t0]\n"                         \
+  "\tv_add_u32_e64 " dd ", " d ", " hh "\n"                             \
   "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                           \
   "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                          \
   "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                          \
-  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                           \
-  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                          \
-  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                          \
   "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"             \
-  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"             \
-  "\tv_add_u32_e64 " hh ", " h ", " KW "\n"                             \
-  "\tv_add3_u32 " hh ", " hh ", %[t5], %[t0]\n"                         \
-  "\tv_add_u32_e64 " dd ", " d ", " hh "\n"                             \
   "\tv_add3_u32 " hh ", " hh ", %[t2], %[t1]\n"
 #define POW_R(a, b, c, d, e, f, g, h, KW) POW_RX(a, b, c, d, e, f, g, h, d, h, KW)
 #define POW_PHASE "\t.p2align 3\n\ts_nop 0\n"
@@ -121,31 +127,39 @@ __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { rou
   [t0] "=&v"(x0), [t1] "=&v"(x1), [t2] "=&v"(x2), [t3] "=&v"(x3), [t4] "=&v"(x4), [t5] "=&v"(x5),   \
       [t6] "=&v"(x6), [t7] "=&v"(x7)
 // Chunk 0's rounds, K+W (or K) from SGPRs (scalar loads of the template
-// constants), W per lane.  The additions keep hipcc's forms (and rates):
+// constants), W per lane, in the same e-path-first order.  The additions keep
+// hipcc's forms (and rates):
 //   rounds 4-15, K+W uniform:  h' = h + Ch (full rate);  T1 = h' + S1 + KW (v_add3, SGPR)
 //   rounds 16-63, K uniform, W per lane: T1 = Ch + h + S1; T1 += K + W (two v_add3, SGPR)
-#define POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                         \
+#define POW_R_KWS(a, b, c, d, e, f, g, h, KWS)                          \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                         \
   "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"           \
   "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"           \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                        \
+  "\tv_add_u32_e64 " h ", " h ", %[t0]\n"                             \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                        \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"           \
+  "\tv_add3_u32 " h ", " h ", %[t5], " KWS "\n"                       \
+  "\tv_add_u32_e64 " d ", " d ", " h "\n"                             \
   "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                         \
   "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                        \
   "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                        \
-  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                         \
-  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                        \
-  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                        \
   "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"           \
-  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"
-#define POW_R_KWS(a, b, c, d, e, f, g, h, KWS)                          \
-  POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                               \
-  "\tv_add_u32_e64 " h ", " h ", %[t0]\n"                             \
-  "\tv_add3_u32 " h ", " h ", %[t5], " KWS "\n"                       \
-  "\tv_add_u32_e64 " d ", " d ", " h "\n"                             \
   "\tv_add3_u32 " h ", %[t2], %[t1], " h "\n"
 #define POW_R_KS_W(a, b, c, d, e, f, g, h, KS, W)                       \
-  POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                               \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                         \
+  "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"           \
+  "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"           \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                        \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                        \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"           \
   "\tv_add3_u32 " h ", %[t0], " h ", %[t5]\n"                         \
   "\tv_add3_u32 " h ", " h ", " KS ", " W "\n"                        \
   "\tv_add_u32_e64 " d ", " d ", " h "\n"                             \
+  "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                         \
+  "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                        \
+  "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                        \
+  "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"           \
   "\tv_add3_u32 " h ", %[t2], %[t1], " h "\n"
 #define POW_STATE_OPS                                                                             \
   [a] "+v"(s.a), [b] "+v"(s.b), [c] "+v"(s.c), [d] "+v"(s.d), [e] "+v"(s.e), [f] "+v"(s.f),        \
@@ -166,10 +180,19 @@ __device__ __forceinline__ void rounds4_kws_asm(St& s, uint32_t k0, uint32_t k1,
 // the per-prefix state, live across the j-loop) without writing it: each
 // state word is written once, into a fresh register (no copies).
 #define POW_R_KWS_X(a, b, c, d, e, f, g, h, dd, hh, KWS)                 \
-  POW_ROUND_HEAD(a, b, c, d, e, f, g, h)                               \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                         \
+  "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"           \
+  "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"           \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                        \
   "\tv_add_u32_e64 " hh ", " h ", %[t0]\n"                            \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                        \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"           \
   "\tv_add3_u32 " hh ", " hh ", %[t5], " KWS "\n"                     \
   "\tv_add_u32_e64 " dd ", " d ", " hh "\n"                           \
+  "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                         \
+  "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                        \
+  "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                        \
+  "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"           \
   "\tv_add3_u32 " hh ", %[t2], %[t1], " hh "\n"
 __device__ __forceinline__ St rounds4_kws_asm_from(const St& in, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
