@@ -9,8 +9,11 @@
  * ran after A returned.  Exit status 0 iff B stopped early and A's block
  * solves.  Used by tools/host_sanitize.sh (ASan/UBSan and TSan runs).
  *
- *   cc -I include examples/board_two_ctx.c -L mpi_blockchain_amd -lpow_gpu -lpthread
- *   POW_GRID_PER_CU=4 ./a.out     (B leaves half the workgroup slots to A)
+ * On one GPU the two contexts share the chip, so the test run links the test
+ * build (libpow_gpu_test.so), whose POW_GRID_PER_CU switch sizes B's grid to
+ * half the workgroup slots; across two GPUs the shipped library needs none:
+ *   cc -I include examples/board_two_ctx.c -L mpi_blockchain_amd -lpow_gpu_test -lpthread
+ *   POW_GRID_PER_CU=4 ./a.out
  */
 #include <pthread.h>
 #include <stdio.h>

@@ -11,6 +11,9 @@ import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libpow_gpu.so")
+# The same library built with -DPOW_TEST_HOOKS (build.py): test and tuning
+# switches read from the environment at pow_init.  Only tests load it.
+TEST_LIB_PATH = os.path.join(PKG, "libpow_gpu_test.so")
 
 HASH_SIZE = 256
 NONCE_SIZE = 10
@@ -66,17 +69,19 @@ POW_VALU_MIX, POW_VALU_FULL, POW_VALU_HALF = 0, 1, 2
 
 assert ctypes.sizeof(Block) == 552
 
-_lib = None
+_libs: dict = {}
 
 
-def load() -> ctypes.CDLL:
-    """Load libpow_gpu.so (raises if it is missing — no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load(test_hooks: bool = False) -> ctypes.CDLL:
+    """Load libpow_gpu.so (raises if it is missing — no fallback).
+    test_hooks=True: libpow_gpu_test.so, the same code plus the test switches
+    (tests only; both may be loaded in one process, each with its own handle)."""
+    path = TEST_LIB_PATH if test_hooks else LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -m mpi_blockchain_amd.build` "
+            f"{path} is missing: build it with `python -m mpi_blockchain_amd.build` "
             "(the GPU path has no CPU fallback)")
     # One HIP runtime per process: when PyTorch-ROCm is importable, load it
     # first so this library binds to the same libamdhip64.so.7 (same soname).
@@ -84,7 +89,7 @@ def load() -> ctypes.CDLL:
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is optional for the C ABI
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P = ctypes.POINTER(Block)
     c_u64p = ctypes.POINTER(ctypes.c_uint64)
     c_sizep = ctypes.POINTER(ctypes.c_size_t)
@@ -142,7 +147,7 @@ def load() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -155,7 +160,9 @@ EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_las
            "pow_board_peek")
 
 
-def check(rc: int) -> int:
+def check(rc: int, L: ctypes.CDLL | None = None) -> int:
+    """Raise PowError for rc < 0 with the message of the library that failed
+    (each loaded library keeps its own pow_last_error)."""
     if rc < 0:
-        raise PowError(rc, (load().pow_last_error() or b"").decode(errors="replace"))
+        raise PowError(rc, ((L or load()).pow_last_error() or b"").decode(errors="replace"))
     return rc

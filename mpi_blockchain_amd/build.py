@@ -34,25 +34,86 @@ def _inputs() -> list[str]:
     return [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + INCLUDES
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+# Test build: the same kernels and API with -DPOW_TEST_HOOKS, i.e. the test and
+# tuning switches read from the environment at pow_init (POW_FORCE_FULL,
+# POW_FAULT_INJECT, POW_LAT_MAX, POW_LAT_WPS, POW_GRID_PER_CU) and the RCCL
+# library override (POW_TEST_RCCL_LIB, tests/stub_rccl).  The shipped
+# libpow_gpu.so has none of them; only tests load this one.
+TEST_LIB = os.path.join(PKG, "libpow_gpu_test.so")
+OBJ = os.path.join(ROOT, "build", "obj")  # git- and gpurun-ignored: the .so files travel, not the objects
+HOOKED = ("pow_api.cpp", "pow_group.cpp")  # the sources that differ between the two builds
+
+
+def _flags() -> list[str]:
+    return [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-mcode-object-version=5", "-Wall",
+            "-Werror=return-type", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+
+
+def up_to_date(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return False
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     return all(os.path.getmtime(p) <= t for p in _inputs())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-mcode-object-version=5", "-Wall", "-Werror=return-type",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+def _compile(src: str, obj: str, defs: tuple[str, ...], verbose: bool) -> None:
+    if os.path.exists(obj) and all(os.path.getmtime(p) <= os.path.getmtime(obj) for p in _inputs()):
+        return
+    cmd = [hipcc(), *_flags(), *defs, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=ROOT)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(obj + ".tmp", obj)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """libpow_gpu.so (shipped) and libpow_gpu_test.so (tests).  Every source
+    is compiled once; pow_api.cpp and pow_group.cpp once more with
+    -DPOW_TEST_HOOKS for the test library."""
+    if not force and up_to_date(LIB) and up_to_date(TEST_LIB):
+        return LIB
+    os.makedirs(OBJ, exist_ok=True)
+    if force:
+        for f in os.listdir(OBJ):
+            os.remove(os.path.join(OBJ, f))
+    common, plain, hooked = [], [], []
+    for s in SOURCES:
+        base = os.path.splitext(s)[0]
+        if s in HOOKED:
+            plain.append(os.path.join(OBJ, base + ".o"))
+            hooked.append(os.path.join(OBJ, base + ".test.o"))
+            _compile(s, plain[-1], (), verbose)
+            _compile(s, hooked[-1], ("-DPOW_TEST_HOOKS",), verbose)
+        else:
+            common.append(os.path.join(OBJ, base + ".o"))
+            _compile(s, common[-1], (), verbose)
+    for lib, objs in ((LIB, plain), (TEST_LIB, hooked)):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *common, *objs, "-o", lib + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=ROOT)
+        os.replace(lib + ".tmp", lib)
     return LIB
+
+
+STUB_SRC = os.path.join(ROOT, "tests", "stub_rccl", "stub_rccl.cpp")
+STUB_LIB = os.path.join(ROOT, "tests", "stub_rccl", "libstub_rccl.so")
+
+
+def build_test_stub(force: bool = False, verbose: bool = False) -> str:
+    """Test infrastructure: the stand-in RCCL (shared-memory reduction) that the
+    TEST library loads through POW_TEST_RCCL_LIB, so pow_group_init runs with
+    several ranks on one GPU (tests/test_shard_gpu.py)."""
+    if not force and os.path.exists(STUB_LIB) and os.path.getmtime(STUB_SRC) <= os.path.getmtime(STUB_LIB):
+        return STUB_LIB
+    cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__",
+           "-I", "/opt/rocm/include", STUB_SRC, "-o", STUB_LIB + ".tmp", "-L", "/opt/rocm/lib", "-lamdhip64",
+           "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=ROOT)
+    os.replace(STUB_LIB + ".tmp", STUB_LIB)
+    return STUB_LIB
 
 
 MPI_HOME = os.environ.get("POW_MPI_HOME", "/opt/conda")  # the image's MPICH (mpi.h, libmpi.so)
@@ -100,3 +161,4 @@ if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_node(force="--force" in sys.argv, verbose=True))
     print(build_node(force="--force" in sys.argv, verbose=True, test=True))
+    print(build_test_stub(force="--force" in sys.argv, verbose=True))

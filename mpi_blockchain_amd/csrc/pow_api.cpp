@@ -211,10 +211,11 @@ struct pow_ctx {
   uint32_t* d_dig = nullptr;
   size_t hash_cap = 0;
   unsigned grid_full = 0;  // workgroups that fill the chip (8 per CU)
-  bool force_full = false; // POW_FORCE_FULL=1: use the d > 32 kernel for every d (tests)
-  bool fault_mine = false;  // POW_FAULT_INJECT=mine: every pow_mine[_any] call fails (failure-propagation tests)
-  uint64_t lat_max = 1ull << 24;  // POW_LAT_MAX: first-sub-round cap for K1' (0 = K1 only)
-  unsigned lat_wps = 0;           // POW_LAT_WPS (tuning runs): K1' waves per SIMD at every d (0 = plan)
+  // Set only by the test library's hooks (POW_TEST_HOOKS, pow_init):
+  bool force_full = false;        // use the d > 32 kernel for every d
+  bool fault_mine = false;        // every pow_mine[_any] call fails (failure-propagation tests)
+  uint64_t lat_max = 1ull << 24;  // first-sub-round cap for K1' (0 = K1 only)
+  unsigned lat_wps = 0;           // K1' waves per SIMD at every d (0 = the plan)
   pow_stats stats{};
 };
 
@@ -482,6 +483,9 @@ int pow_init(int device, pow_ctx** out) {
   // that a K2 launch (block validation on another stream/context, 40 VGPRs)
   // can run beside a K1 launch instead of waiting up to its whole ~0.13 s.
   ctx->grid_full = (unsigned)prop.multiProcessorCount * 8u - 1u;
+#ifdef POW_TEST_HOOKS
+  // Test and tuning switches: compiled only into libpow_gpu_test.so
+  // (mpi_blockchain_amd/build.py), never into the shipped libpow_gpu.so.
   if (const char* ff = getenv("POW_FORCE_FULL")) ctx->force_full = ff[0] == '1';
   if (const char* fi = getenv("POW_FAULT_INJECT")) ctx->fault_mine = std::strcmp(fi, "mine") == 0;
   if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
@@ -490,6 +494,7 @@ int pow_init(int device, pow_ctx** out) {
     const int per = atoi(g);
     if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
   }
+#endif
   int rc = POW_OK;
   auto chk = [&](hipError_t e, const char* what) {
     if (e != hipSuccess && rc == POW_OK) rc = fail(POW_EHIP, "%s: %s", what, hipGetErrorString(e));
@@ -795,7 +800,9 @@ static int mine_impl(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
   if (int rc = set_dev(ctx)) return rc;
   ctx->stats = pow_stats{};
   if (hashes_done) *hashes_done = 0;
+#ifdef POW_TEST_HOOKS
   if (ctx->fault_mine) return fail(POW_EHIP, "injected fault (POW_FAULT_INJECT=mine)");
+#endif
   if (int rc = upload_consts(ctx, tmpl)) return rc;
   ctx->launch_epoch = epoch;
   ctx->watch_epoch = cancel_word != nullptr;

@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/pow_gpu.h"
@@ -54,8 +55,19 @@ const Rccl& rccl() {
   static const Rccl r = [] {
     Rccl x;
     void* h = nullptr;
+#ifdef POW_TEST_HOOKS
+    // Test library only: a stand-in RCCL (tests/stub_rccl) that reduces over
+    // POSIX shared memory, so pow_group_init's RCCL leg runs with several
+    // ranks on the one GPU of a test box (RCCL refuses two ranks per GPU).
+    if (const char* p = getenv("POW_TEST_RCCL_LIB")) {
+      if (!(h = dlopen(p, RTLD_NOW | RTLD_LOCAL))) {
+        snprintf(x.why, sizeof x.why, "cannot load POW_TEST_RCCL_LIB %s: %s", p, dlerror());
+        return x;
+      }
+    }
+#endif
     for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
-      if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+      if (h || (h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
     if (!h) {
       snprintf(x.why, sizeof x.why, "cannot load RCCL: %s", dlerror());
       return x;

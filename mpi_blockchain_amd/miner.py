@@ -41,16 +41,19 @@ def refresh_template(last: Block, rank: int, difficulty: int = DEFAULT_DIFFICULT
 
 
 class GpuMiner:
-    def __init__(self, device: int = 0):
-        self.L = load()
+    def __init__(self, device: int = 0, test_hooks: bool = False):
+        """test_hooks=True: a context of libpow_gpu_test.so, which reads the
+        test switches (POW_FORCE_FULL, POW_LAT_MAX, POW_GRID_PER_CU, ...) from
+        the environment at pow_init; tests only."""
+        self.L = load(test_hooks)
         self.ctx = ctypes.c_void_p()
-        check(self.L.pow_init(device, ctypes.byref(self.ctx)))
+        check(self.L.pow_init(device, ctypes.byref(self.ctx)), self.L)
         self.device = device
         self._cancel = ctypes.c_uint32(0)
 
     def warmup(self) -> None:
         """Load every kernel now (HIP loads code objects at first launch)."""
-        check(self.L.pow_warmup(self.ctx))
+        check(self.L.pow_warmup(self.ctx), self.L)
 
     # ---- lifecycle ----
     def close(self) -> None:
@@ -74,12 +77,12 @@ class GpuMiner:
     def device_info(self) -> dict:
         cu, clk = ctypes.c_int(), ctypes.c_int()
         name = ctypes.create_string_buffer(256)
-        check(self.L.pow_device_info(self.ctx, ctypes.byref(cu), ctypes.byref(clk), name, 256))
+        check(self.L.pow_device_info(self.ctx, ctypes.byref(cu), ctypes.byref(clk), name, 256), self.L)
         return {"cu_count": cu.value, "clock_khz": clk.value, "name": name.value.decode()}
 
     def stats(self) -> dict:
         s = PowStats()
-        check(self.L.pow_get_stats(self.ctx, ctypes.byref(s)))
+        check(self.L.pow_get_stats(self.ctx, ctypes.byref(s)), self.L)
         return {"kernel_ms": s.kernel_ms, "launches": s.launches, "hashes": s.hashes}
 
     # ---- block_to_hash (block.cpp:74-77) ----
@@ -89,7 +92,7 @@ class GpuMiner:
             return []
         arr = (Block * n)(*blocks)
         hx = ctypes.create_string_buffer(65 * n)
-        check(self.L.pow_hash_blocks(self.ctx, arr, n, None, hx))
+        check(self.L.pow_hash_blocks(self.ctx, arr, n, None, hx), self.L)
         raw = hx.raw
         return [raw[65 * i: 65 * i + 64].decode() for i in range(n)]
 
@@ -98,7 +101,7 @@ class GpuMiner:
 
     def digest(self, b: Block) -> bytes:
         dg = ctypes.create_string_buffer(32)
-        check(self.L.pow_hash_block(self.ctx, ctypes.byref(b), dg, None))
+        check(self.L.pow_hash_block(self.ctx, ctypes.byref(b), dg, None), self.L)
         return dg.raw
 
     # ---- mining ----
@@ -108,7 +111,7 @@ class GpuMiner:
         running mine call stops within one inner step, not at its next
         sub-round."""
         self._cancel.value = (self._cancel.value + 1) & 0xFFFFFFFF
-        check(self.L.pow_cancel(self.ctx, self._cancel.value))
+        check(self.L.pow_cancel(self.ctx, self._cancel.value), self.L)
 
     @property
     def epoch(self) -> int:
@@ -119,7 +122,7 @@ class GpuMiner:
         this miner's hits go to `slot` of `board`, and its mine calls stop as
         soon as a peer slot of the same `tag` makes its remaining counters
         moot.  board=None unbinds."""
-        check(self.L.pow_board_bind(self.ctx, board.ptr if board is not None else None, slot, tag))
+        check(self.L.pow_board_bind(self.ctx, board.ptr if board is not None else None, slot, tag), self.L)
 
     def mine(self, tmpl: Block, start: int = 0, count: int = 1 << 40, difficulty: int = DEFAULT_DIFFICULTY,
              epoch: int | None = None, any_solution: bool = False) -> MineResult | None:
@@ -131,7 +134,7 @@ class GpuMiner:
         fn = self.L.pow_mine_any if any_solution else self.L.pow_mine
         rc = check(fn(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
                       ctypes.byref(self._cancel), ep, ctypes.byref(out),
-                      ctypes.byref(ctr), ctypes.byref(hashes)))
+                      ctypes.byref(ctr), ctypes.byref(hashes)), self.L)
         if rc == 0:
             return None
         return MineResult(out, ctr.value, hashes.value, self.stats()["kernel_ms"])
@@ -143,7 +146,7 @@ class GpuMiner:
         out = np.zeros(max(cap, 1), dtype=np.uint32)
         n = ctypes.c_size_t()
         check(self.L.pow_sweep(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
-                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), cap, ctypes.byref(n)))
+                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), cap, ctypes.byref(n)), self.L)
         return out[: n.value]  # a view: copying 33.6 MB (a 2^32 window at d = 9) again costs ~3 ms
 
     def sweep_count(self, tmpl: Block, start: int, count: int, difficulty: int,
@@ -153,7 +156,7 @@ class GpuMiner:
         ptr = dev_out.ptr if isinstance(dev_out, DeviceBuffer) else dev_out
         check(self.L.pow_sweep_device(self.ctx, ctypes.byref(tmpl), start, count, difficulty,
                                       ptr if ptr else None, cap,
-                                      ctypes.byref(n), ctypes.byref(mn)))
+                                      ctypes.byref(n), ctypes.byref(mn)), self.L)
         return n.value, (None if mn.value == 0xFFFFFFFFFFFFFFFF else mn.value)
 
 
@@ -165,23 +168,23 @@ class StopBoard:
 
     NONE = None
 
-    def __init__(self, nslots: int, name: str | None = None):
-        self.L = load()
+    def __init__(self, nslots: int, name: str | None = None, test_hooks: bool = False):
+        self.L = load(test_hooks)
         self.name = name
         self.ptr = ctypes.c_void_p()
-        check(self.L.pow_board_open(name.encode() if name else None, nslots, ctypes.byref(self.ptr)))
+        check(self.L.pow_board_open(name.encode() if name else None, nslots, ctypes.byref(self.ptr)), self.L)
 
     def post(self, slot: int, tag: int, counter: int | None) -> None:
-        check(self.L.pow_board_post(self.ptr, slot, tag, 0xFFFFFFFFFFFFFFFF if counter is None else counter))
+        check(self.L.pow_board_post(self.ptr, slot, tag, 0xFFFFFFFFFFFFFFFF if counter is None else counter), self.L)
 
     def peek(self, except_slot: int, tag: int) -> int | None:
         v = ctypes.c_uint64()
-        check(self.L.pow_board_peek(self.ptr, except_slot, tag, ctypes.byref(v)))
+        check(self.L.pow_board_peek(self.ptr, except_slot, tag, ctypes.byref(v)), self.L)
         return None if v.value == 0xFFFFFFFFFFFFFFFF else v.value
 
     def unlink(self) -> None:
         if self.name:
-            check(self.L.pow_board_unlink(self.name.encode()))
+            check(self.L.pow_board_unlink(self.name.encode()), self.L)
 
     def close(self) -> None:
         if self.ptr:
@@ -201,18 +204,18 @@ class DeviceBuffer:
     def __init__(self, miner: "GpuMiner", nbytes: int):
         self.miner, self.nbytes = miner, nbytes
         self.ptr = ctypes.c_void_p()
-        check(miner.L.pow_dev_alloc(miner.ctx, nbytes, ctypes.byref(self.ptr)))
+        check(miner.L.pow_dev_alloc(miner.ctx, nbytes, ctypes.byref(self.ptr)), miner.L)
 
     def read_u32(self, n: int) -> np.ndarray:
         out = np.zeros(n, dtype=np.uint32)
         if n:
             check(self.miner.L.pow_dev_read(self.miner.ctx, self.ptr, out.ctypes.data_as(ctypes.c_void_p),
-                                            4 * n))
+                                            4 * n), self.miner.L)
         return out
 
     def free(self) -> None:
         if self.ptr:
-            check(self.miner.L.pow_dev_free(self.miner.ctx, self.ptr))
+            check(self.miner.L.pow_dev_free(self.miner.ctx, self.ptr), self.miner.L)
             self.ptr = ctypes.c_void_p()
 
 

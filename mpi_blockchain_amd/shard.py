@@ -54,13 +54,14 @@ class _Group:
     """A ``pow_group``: the collective sharded search of include/pow_gpu.h."""
 
     miner = None
+    L = None  # the library that made the group (the miner's)
     g = ctypes.c_void_p()
 
     def allreduce(self, vals, op: str = "min") -> list[int]:
         """In-place all-reduce of <= 8 uint64 over the group's ranks."""
         arr = (ctypes.c_uint64 * len(vals))(*vals)
         code = {"min": POW_REDUCE_MIN, "max": POW_REDUCE_MAX, "sum": POW_REDUCE_SUM}[op]
-        check(load().pow_group_allreduce_u64(self.g, arr, len(vals), code))
+        check(self.L.pow_group_allreduce_u64(self.g, arr, len(vals), code), self.L)
         return list(arr)
 
     def mine(self, tmpl, start: int, count: int, difficulty: int, round_size: int = 0,
@@ -81,14 +82,14 @@ class _Group:
         fn = m.L.pow_group_mine_any if any_solution else m.L.pow_group_mine
         rc = check(fn(self.g, ctypes.byref(tmpl), start, count, round_size, difficulty,
                       ctypes.byref(m._cancel), ep, ctypes.byref(out), ctypes.byref(ctr),
-                      ctypes.byref(hashes)))
+                      ctypes.byref(hashes)), self.L)
         if rc == 0:
             return None
         return MineResult(out, ctr.value, hashes.value, m.stats()["kernel_ms"])
 
     def close(self) -> None:
         if self.g:
-            load().pow_group_destroy(self.g)
+            self.L.pow_group_destroy(self.g)
             self.g = ctypes.c_void_p()
 
     def __enter__(self):
@@ -110,15 +111,19 @@ class RcclGroup(_Group):
         if len(unique_id) != GROUP_ID_BYTES:
             raise ValueError("unique_id must be 128 bytes")
         self.miner, self.rank, self.world = miner, rank, world
+        self.L = miner.L
         self.g = ctypes.c_void_p()
-        check(miner.L.pow_group_init(miner.ctx, world, rank, unique_id, ctypes.byref(self.g)))
+        check(miner.L.pow_group_init(miner.ctx, world, rank, unique_id, ctypes.byref(self.g)), miner.L)
 
     @staticmethod
-    def make_unique_id() -> bytes:
+    def make_unique_id(L: ctypes.CDLL | None = None) -> bytes:
+        """A fresh 128-byte id (ncclGetUniqueId) from library `L` (default:
+        the shipped one; pass a miner's ``L`` to match its library)."""
         from ._lib import GROUP_ID_BYTES
 
+        L = L or load()
         buf = ctypes.create_string_buffer(GROUP_ID_BYTES)
-        check(load().pow_group_unique_id(buf))
+        check(L.pow_group_unique_id(buf), L)
         return buf.raw
 
     @classmethod
@@ -132,7 +137,7 @@ class RcclGroup(_Group):
         obj = [None]
         if dist.get_rank(group) == 0:
             try:
-                obj[0] = cls.make_unique_id()
+                obj[0] = cls.make_unique_id(miner.L)
             except Exception as e:
                 obj[0] = f"rank 0: {e}"
         dist.broadcast_object_list(obj, src=0, group=group)
@@ -176,6 +181,7 @@ class ShardedMiner(_Group):
         import torch.distributed as dist
 
         self.miner, self.rank, self.world = miner, rank, world
+        self.L = miner.L if miner is not None else load()
         self.g = ctypes.c_void_p()
         self.reduce_error: Exception | None = None
         red = torch_reduction(device, group)
@@ -196,5 +202,5 @@ class ShardedMiner(_Group):
             obj = [f"/pow_board_{os.getpid()}_{uuid.uuid4().hex[:12]}" if dist.get_rank(group) == 0 else None]
             dist.broadcast_object_list(obj, src=0, group=group)
             name = obj[0]
-        check(load().pow_group_init_custom(miner.ctx if miner is not None else None, world, rank, self._cb, None,
-                                           name.encode() if name else None, ctypes.byref(self.g)))
+        check(self.L.pow_group_init_custom(miner.ctx if miner is not None else None, world, rank, self._cb, None,
+                                           name.encode() if name else None, ctypes.byref(self.g)), self.L)

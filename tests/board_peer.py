@@ -22,7 +22,8 @@ from mpi_blockchain_amd.miner import GpuMiner, StopBoard  # noqa: E402
 
 def main():
     name, slot, tag = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    with GpuMiner(0) as m, StopBoard(2, name) as board:
+    # the test library: POW_GRID_PER_CU (set by the caller) leaves half the chip to the finder
+    with GpuMiner(0, test_hooks=True) as m, StopBoard(2, name) as board:
         m.warmup()
         m.bind_board(board, slot, tag)
         print("ready", flush=True)

@@ -1,0 +1,189 @@
+// TEST INFRASTRUCTURE ONLY: a stand-in for the five RCCL entry points that
+// mpi_blockchain_amd/csrc/pow_group.cpp dlopens (rccl.h:187, 220, 260, 339,
+// 611), reducing over POSIX shared memory instead of xGMI.
+//
+// RCCL refuses two ranks on one GPU, and a test box has one GPU, so
+// pow_group_init's RCCL leg (the board opened before ncclCommInitRank and
+// unlinked after it, the d_buf/h_buf staging around ncclAllReduce, the
+// {counter, go, ok} consensus) could only run at world size 1.  With this
+// library selected by the TEST build's hook (libpow_gpu_test.so,
+// POW_TEST_RCCL_LIB) the very same pow_group code runs with 2 and 4 processes
+// sharing the GPU (tests/test_shard_gpu.py).  Built by build.build_test_stub();
+// never loaded by the shipped libpow_gpu.so, which has no such hook.
+//
+// Semantics kept from RCCL: ncclCommInitRank blocks until all nranks joined;
+// ncclAllReduce takes device buffers and is ordered on the caller's stream
+// (the stub synchronises the stream, reduces on the host, and writes the
+// result back on the same stream).  Only what pow_group uses is supported:
+// ncclUint64, min/max/sum, at most 8 words per call.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+namespace {
+
+constexpr int kMaxRanks = 64;
+constexpr size_t kMaxWords = 8;
+constexpr char kMagic[8] = {'p', 'o', 'w', 's', 't', 'u', 'b', '1'};
+constexpr double kTimeoutS = 120.0;  // a rank that never arrives fails the call, it does not hang the test
+
+struct Shared {
+  std::atomic<uint32_t> joined;
+  std::atomic<uint32_t> arrive;  // central barrier: arrivals of the current phase ...
+  std::atomic<uint32_t> phase;   // ... and the phase number (bumped by the last arrival)
+  uint64_t slot[kMaxRanks][kMaxWords];
+};
+
+std::atomic<uint64_t> g_allreduce_calls{0};
+
+double now_s() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+void pause_us(long us) {
+  timespec t{0, us * 1000};
+  nanosleep(&t, nullptr);
+}
+
+void shm_name(const ncclUniqueId& id, char out[48]) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the id
+  for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; ++i) h = (h ^ (uint8_t)id.internal[i]) * 1099511628211ull;
+  snprintf(out, 48, "/pow_stub_rccl_%016llx", (unsigned long long)h);
+}
+
+}  // namespace
+
+struct ncclComm {
+  Shared* sh = nullptr;
+  int nranks = 0, rank = 0;
+};
+
+namespace {
+
+bool barrier(ncclComm* c) {
+  Shared* s = c->sh;
+  const uint32_t ph = s->phase.load(std::memory_order_acquire);
+  if (s->arrive.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)c->nranks) {
+    s->arrive.store(0, std::memory_order_relaxed);
+    s->phase.fetch_add(1, std::memory_order_acq_rel);
+    return true;
+  }
+  const double t0 = now_s();
+  while (s->phase.load(std::memory_order_acquire) == ph) {
+    if (now_s() - t0 > kTimeoutS) return false;
+    pause_us(20);
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+// How many all-reduces this process ran through the stub (tests check that the
+// stub, not RCCL, carried the group's collectives).
+uint64_t pow_stub_rccl_allreduce_calls(void) { return g_allreduce_calls.load(); }
+
+ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
+  if (!id) return ncclInvalidArgument;
+  const int fd = open("/dev/urandom", O_RDONLY);
+  if (fd < 0) return ncclSystemError;
+  const ssize_t n = read(fd, id->internal, sizeof id->internal);
+  close(fd);
+  if (n != (ssize_t)sizeof id->internal) return ncclSystemError;
+  memcpy(id->internal, kMagic, sizeof kMagic);
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank) {
+  if (!comm || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+  if (memcmp(id.internal, kMagic, sizeof kMagic) != 0) return ncclInvalidArgument;  // not a stub id
+  *comm = nullptr;
+  char name[48];
+  shm_name(id, name);
+  const int fd = shm_open(name, O_RDWR | O_CREAT, 0600);
+  if (fd < 0) return ncclSystemError;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (st.st_size < (off_t)sizeof(Shared) && ftruncate(fd, sizeof(Shared)) != 0)) {
+    close(fd);
+    return ncclSystemError;
+  }
+  void* p = mmap(nullptr, sizeof(Shared), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return ncclSystemError;
+  ncclComm* c = new ncclComm;
+  c->sh = (Shared*)p;  // a fresh object is zero-filled: all counters 0
+  c->nranks = nranks;
+  c->rank = rank;
+  // As RCCL: return once every rank has joined.
+  c->sh->joined.fetch_add(1, std::memory_order_acq_rel);
+  const double t0 = now_s();
+  while (c->sh->joined.load(std::memory_order_acquire) < (uint32_t)nranks) {
+    if (now_s() - t0 > kTimeoutS) {
+      munmap(p, sizeof(Shared));
+      delete c;
+      return ncclSystemError;
+    }
+    pause_us(50);
+  }
+  shm_unlink(name);  // every rank has it mapped; nothing is left in /dev/shm
+  *comm = c;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  munmap(comm->sh, sizeof(Shared));
+  delete comm;
+  return ncclSuccess;
+}
+
+const char* ncclGetErrorString(ncclResult_t r) {
+  switch (r) {
+    case ncclSuccess: return "no error (stub RCCL)";
+    case ncclInvalidArgument: return "invalid argument (stub RCCL)";
+    case ncclSystemError: return "system error or timeout (stub RCCL)";
+    case ncclUnhandledCudaError: return "HIP error (stub RCCL)";
+    default: return "unsupported (stub RCCL)";
+  }
+}
+
+ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                           ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+  if (!comm || datatype != ncclUint64 || count > kMaxWords) return ncclInvalidArgument;
+  if (op != ncclMin && op != ncclMax && op != ncclSum) return ncclInvalidArgument;
+  uint64_t v[kMaxWords] = {0};
+  // The operand was staged on `stream` (pow_group: hipMemcpyAsync H2D): wait for it.
+  if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
+  if (count && hipMemcpy(v, sendbuff, count * 8, hipMemcpyDeviceToHost) != hipSuccess) return ncclUnhandledCudaError;
+  Shared* s = comm->sh;
+  memcpy(s->slot[comm->rank], v, count * 8);
+  if (!barrier(comm)) return ncclSystemError;  // every rank's words are in
+  uint64_t r[kMaxWords];
+  memcpy(r, s->slot[0], count * 8);
+  for (int k = 1; k < comm->nranks; ++k)
+    for (size_t i = 0; i < count; ++i) {
+      const uint64_t x = s->slot[k][i];
+      r[i] = op == ncclMin ? (x < r[i] ? x : r[i]) : op == ncclMax ? (x > r[i] ? x : r[i]) : r[i] + x;
+    }
+  if (!barrier(comm)) return ncclSystemError;  // every rank has read them: the slots may be reused
+  if (count && hipMemcpyAsync(recvbuff, r, count * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
+    return ncclUnhandledCudaError;
+  if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
+  g_allreduce_calls.fetch_add(1);
+  return ncclSuccess;
+}
+
+}  // extern "C"

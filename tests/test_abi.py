@@ -38,6 +38,25 @@ def test_library_exports_all_symbols():
         assert hasattr(L, name), name
 
 
+HOOKS = (b"POW_FAULT_INJECT", b"POW_FORCE_FULL", b"POW_LAT_MAX", b"POW_LAT_WPS", b"POW_GRID_PER_CU",
+         b"POW_TEST_RCCL_LIB")
+
+
+def test_shipped_library_has_no_test_hooks():
+    """The test and tuning switches (fault injection, forced kernel variants,
+    launch geometry, the stand-in RCCL) exist only in libpow_gpu_test.so,
+    built from the same objects plus -DPOW_TEST_HOOKS (build.py); the shipped
+    libpow_gpu.so reads no such variable.  Both export the same ABI."""
+    shipped = open(_lib.LIB_PATH, "rb").read()
+    test = open(_lib.TEST_LIB_PATH, "rb").read()
+    assert [h for h in HOOKS if h in shipped] == []
+    assert all(h in test for h in HOOKS)
+    T = _lib.load(test_hooks=True)
+    assert T is not _lib.load()
+    for name in header_functions():
+        assert hasattr(T, name), name
+
+
 def test_block_layout():
     assert ctypes.sizeof(_lib.Block) == 552
     assert _lib.Block.nonce.offset == 24 and _lib.Block.block_hash.offset == 290

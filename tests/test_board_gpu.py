@@ -5,8 +5,9 @@ BASELINE config 4 asks for winner selection AND cancellation across GPUs.
 These tests drive two contexts on the one GPU of the box (in one process, and
 in two processes through POSIX shared memory): the mechanism is the same as
 across the GPUs of a node, since every GPU reads the board over PCIe.  The
-running context is created with POW_GRID_PER_CU=4 so that it leaves half the
-workgroup slots free and the finder's launch runs beside it.
+running context is created with POW_GRID_PER_CU=4 (a switch of the test
+library, libpow_gpu_test.so) so that it leaves half the workgroup slots free
+and the finder's launch runs beside it.
 """
 import json
 import os
@@ -34,11 +35,13 @@ def s0():
 
 
 def half_grid_miner():
+    """A context of the test library (libpow_gpu_test.so) whose K1 grid is 4
+    workgroups per CU (POW_GRID_PER_CU, a test-build switch)."""
     from mpi_blockchain_amd.miner import GpuMiner
 
     os.environ["POW_GRID_PER_CU"] = "4"
     try:
-        m = GpuMiner(0)
+        m = GpuMiner(0, test_hooks=True)
     finally:
         del os.environ["POW_GRID_PER_CU"]
     m.warmup()

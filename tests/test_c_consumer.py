@@ -73,7 +73,8 @@ def board_exe(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("cb") / "board_two_ctx")
     subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-D_POSIX_C_SOURCE=200809L", "-I",
                     os.path.join(ROOT, "include"), os.path.join(ROOT, "examples", "board_two_ctx.c"), "-L", PKG,
-                    "-lpow_gpu", f"-Wl,-rpath,{PKG}", "-lpthread", "-o", out], check=True)
+                    # the test library: POW_GRID_PER_CU=4 (a test-build switch) leaves half the chip to A
+                    "-lpow_gpu_test", f"-Wl,-rpath,{PKG}", "-lpthread", "-o", out], check=True)
     return out
 
 

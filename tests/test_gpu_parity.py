@@ -31,14 +31,25 @@ def miner():
     m.close()
 
 
+def hooked_miner(**env) -> GpuMiner:
+    """A context of the test library (libpow_gpu_test.so) with test switches
+    set for its pow_init; the shipped library has none of them."""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return GpuMiner(0, test_hooks=True)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 @pytest.fixture(scope="module")
 def miner_full():
     """A context whose every launch uses the d > 32 kernel variant."""
-    os.environ["POW_FORCE_FULL"] = "1"
-    try:
-        m = GpuMiner(0)
-    finally:
-        os.environ.pop("POW_FORCE_FULL", None)
+    m = hooked_miner(POW_FORCE_FULL=1)
     yield m
     m.close()
 
@@ -46,11 +57,7 @@ def miner_full():
 @pytest.fixture(scope="module")
 def miner_k1():
     """pow_mine on the throughput kernel only (latency kernel K1' disabled)."""
-    os.environ["POW_LAT_MAX"] = "0"
-    try:
-        m = GpuMiner(0)
-    finally:
-        os.environ.pop("POW_LAT_MAX", None)
+    m = hooked_miner(POW_LAT_MAX=0)
     yield m
     m.close()
 
@@ -472,6 +479,25 @@ def test_parity_fuzz():
         res = parity_fuzz.run(120, 2024, miner=m)
     assert res.get("ok"), res
     assert res["cases"] == 120 and res["solutions"] > 0
+
+
+@pytest.mark.parametrize("env", [{"POW_LAT_WPS": 4}, {"POW_LAT_WPS": 4, "POW_FORCE_FULL": 1}],
+                         ids=["lat_asm", "lat_asm_full"])
+def test_parity_fuzz_latency_asm_variants(env):
+    """The latency kernel's asm-group variants (pow_search_lat<*, *, true>, run
+    by the plan only at d = 20-21, 4 waves per SIMD) under the same exact
+    oracle comparison: the test library forces 4 waves per SIMD at every d,
+    and with POW_FORCE_FULL the d > 32 variants <true, *, true> as well."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import parity_fuzz
+
+    m = hooked_miner(**env)
+    try:
+        res = parity_fuzz.run(40, 4040 + len(env), miner=m)
+    finally:
+        m.close()
+    assert res.get("ok"), res
+    assert res["cases"] == 40 and res["solutions"] > 0
 
 
 def test_sweep_d0_full_window_count():

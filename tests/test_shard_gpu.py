@@ -2,11 +2,16 @@
 
 The C++ rounds, the stop board and the {counter, go, ok} consensus of
 csrc/pow_group.cpp run here with 1, 2 and 4 ranks.  RCCL refuses two ranks on
-one device and this pool gives one GPU per call, so the multi-rank tests
-build the group with pow_group_init_custom over torch.distributed gloo
-(ShardedMiner): every rank is its own process with its own pow_ctx on the one
-GPU, and only the one all-reduce per round changes transport.  RCCL itself
-(pow_group_init) runs at world size 1 below; the 8-GPU run is the driver's.
+one device and this pool gives one GPU per call, so the multi-rank tests run
+every rank as its own process with its own pow_ctx on the one GPU, and the
+one all-reduce per round goes over
+  * pow_group_init_custom + torch.distributed gloo (ShardedMiner), or
+  * pow_group_init itself, whose RCCL calls the test library
+    (libpow_gpu_test.so) routes to a shared-memory stand-in
+    (tests/stub_rccl): the id-derived board name, open-before-init,
+    unlink-after-init and the device staging of the operand all run.
+Real RCCL (pow_group_init) runs at world size 1 below; the 8-GPU run is the
+driver's.
 
 Expected values are golden (tests/golden/fingerprints_2p32.json):
 S0's first solutions at d = 13, 21, 25 are 6399, 2392323 and 73523910."""
@@ -55,8 +60,19 @@ def test_sharded_world1_equals_unsharded():
         dist.destroy_process_group()
 
 
-def _group_rank(rank, world, port, q, fault_rank):
-    """One rank of a multi-process group on the one GPU."""
+def _fnv1a(data: bytes) -> int:
+    h = 1469598103934665603
+    for x in data:
+        h = ((h ^ x) * 1099511628211) & ((1 << 64) - 1)
+    return h
+
+
+def _group_rank(rank, world, port, q, fault_rank, transport="gloo"):
+    """One rank of a multi-process group on the one GPU.  transport "gloo":
+    pow_group_init_custom over torch.distributed (ShardedMiner); "rccl_stub":
+    pow_group_init itself, its RCCL calls served by the test library's
+    stand-in (tests/stub_rccl, POW_TEST_RCCL_LIB)."""
+    import ctypes
     import threading
     import time
 
@@ -65,10 +81,15 @@ def _group_rank(rank, world, port, q, fault_rank):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if rank == fault_rank:
         os.environ["POW_FAULT_INJECT"] = "mine"  # every pow_mine of this rank's context fails
+    stub = transport == "rccl_stub"
+    if stub:
+        from mpi_blockchain_amd.build import STUB_LIB
+
+        os.environ["POW_TEST_RCCL_LIB"] = STUB_LIB
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mpi_blockchain_amd._lib import PowError
     from mpi_blockchain_amd.miner import GpuMiner, block_hex
-    from mpi_blockchain_amd.shard import ShardedMiner
+    from mpi_blockchain_amd.shard import RcclGroup, ShardedMiner
 
     out = {}
     S0 = make_block(1, 0, 9, 1700000000, b"")
@@ -77,9 +98,26 @@ def _group_rank(rank, world, port, q, fault_rank):
         return None if r is None else (r.counter, bytes(r.block.nonce).rstrip(b"\0").decode(), block_hex(r.block),
                                        r.hashes)
 
-    with GpuMiner(0) as m:
+    def make_group(m):
+        if not stub:
+            return ShardedMiner(m, rank, world)
+        # pow_group_init as a C caller uses it: rank 0's id (the stub's
+        # ncclGetUniqueId) reaches every rank, all join ncclCommInitRank
+        obj = [RcclGroup.make_unique_id(m.L) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        g = RcclGroup(m, rank, world, obj[0])
+        # the board (named after the id) was opened before the communicator
+        # and unlinked once it joined, and the stub's segment is gone too
+        h = _fnv1a(obj[0])
+        out["shm_left"] = [p for p in (f"/dev/shm/pow_board_{h:016x}", f"/dev/shm/pow_stub_rccl_{h:016x}")
+                           if os.path.exists(p)]
+        return g
+
+    # the contexts come from the test library where a test switch is needed
+    # (POW_FAULT_INJECT on the faulty rank; the RCCL stand-in on every rank)
+    with GpuMiner(0, test_hooks=stub or rank == fault_rank) as m:
         m.warmup()
-        with ShardedMiner(m, rank, world) as sm:
+        with make_group(m) as sm:
             if fault_rank >= 0:
                 try:
                     sm.mine(S0, 0, 1 << 30, 21)
@@ -108,18 +146,20 @@ def _group_rank(rank, world, port, q, fault_rank):
                 out["cancel_s"] = time.perf_counter() - t
                 # and the group still mines correctly afterwards
                 out["after_cancel"] = res(sm.mine(S0, 0, 1 << 26, 21))
+    if stub:
+        out["stub_allreduces"] = ctypes.CDLL(STUB_LIB).pow_stub_rccl_allreduce_calls()
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run_ranks(world, fault_rank=-1, timeout=240):
+def _run_ranks(world, fault_rank=-1, timeout=240, transport="gloo"):
     import torch.multiprocessing as mp
 
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_group_rank, args=(r, world, port, q, fault_rank)) for r in range(world)]
+    procs = [ctx.Process(target=_group_rank, args=(r, world, port, q, fault_rank, transport)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -133,16 +173,25 @@ def _run_ranks(world, fault_rank=-1, timeout=240):
     return out
 
 
+@pytest.mark.parametrize("transport", ["gloo", "rccl_stub"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_group_multiprocess(world):
+def test_group_multiprocess(world, transport):
     """pow_group_mine / pow_group_mine_any with `world` peer processes (C++
     rounds, stop board shared through POSIX shared memory, the 24-byte
-    consensus through gloo): every rank returns the golden lowest counter with
-    its nonce and hash; any-mode agrees on one solving counter; one rank's
-    cancel makes every rank return None."""
+    consensus): every rank returns the golden lowest counter with its nonce
+    and hash; any-mode agrees on one solving counter; one rank's cancel makes
+    every rank return None.  transport "gloo": pow_group_init_custom over
+    torch.distributed; "rccl_stub": pow_group_init's RCCL leg itself (board
+    named after the id, opened before ncclCommInitRank and unlinked after it,
+    d_buf/h_buf staging around ncclAllReduce), with the test library's
+    shared-memory stand-in for RCCL, which refuses two ranks on one GPU."""
     from mpi_blockchain_amd.block import nonce_from_counter, solves_problem
 
-    out = _run_ranks(world)
+    out = _run_ranks(world, transport=transport)
+    if transport == "rccl_stub":
+        for r in range(world):
+            assert out[r]["shm_left"] == [], out[r]["shm_left"]
+            assert out[r]["stub_allreduces"] >= 10, out[r]["stub_allreduces"]
     for key, ctr, d in (("d21", 2392323, 21), ("d25", 73523910, 25), ("d13_rounds", 6399, 13)):
         vals = {out[r][key][:3] for r in range(world)}
         assert len(vals) == 1, (key, vals)  # the same result on every rank
@@ -159,14 +208,15 @@ def test_group_multiprocess(world):
     assert all(out[r]["after_cancel"][0] == 2392323 for r in range(world))
 
 
-def test_group_failure_propagates():
-    """An injected failure on one rank (POW_FAULT_INJECT=mine: its pow_mine
-    returns POW_EHIP) makes every rank's pow_group_mine fail together: the
+@pytest.mark.parametrize("transport", ["gloo", "rccl_stub"])
+def test_group_failure_propagates(transport):
+    """An injected failure on one rank (POW_FAULT_INJECT=mine in the test
+    library, libpow_gpu_test.so: its pow_mine returns POW_EHIP) makes every rank's pow_group_mine fail together: the
     failing rank with its own error, its peers with POW_ECOMM."""
     from mpi_blockchain_amd._lib import POW_ECOMM, POW_EHIP
 
     world = 2
-    out = _run_ranks(world, fault_rank=1)
+    out = _run_ranks(world, fault_rank=1, transport=transport)
     assert out[1]["fault"][0] == POW_EHIP and "injected fault" in out[1]["fault"][1]
     assert out[0]["fault"][0] == POW_ECOMM and "a peer rank failed" in out[0]["fault"][1]
 
