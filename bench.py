@@ -23,6 +23,10 @@ others through the stop board; one all-reduce agrees on the winner).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Without a launcher, `--gpus N` (N > 1) starts the second form itself as a
+child process and relays its JSON line; a launcher's WORLD_SIZE that differs
+from --gpus, or a failed pow_group_init at N > 1, exits non-zero.
 """
 from __future__ import annotations
 
@@ -260,10 +264,15 @@ def pmc_live(cu_count: int, timeout: float = 120) -> dict:
     out["valu"] = {"counters": c, "kernel_ns": t_ns, "dispatches": len(per),
                    "valu_instr_per_hash": round(c["SQ_INSTS_VALU"] * 64 / WINDOW, 1),
                    "clock_ghz": round(clock / 1e9, 4),
-                   # counter_defs.yaml's VALUBusy (gfx94x formula: every VALU
-                   # instruction priced at 4 cycles of one SIMD), > 100 % on
-                   # gfx950's SIMD-32, where a full-rate instruction takes 2
-                   "valu_busy_pct": round(100 * c["SQ_ACTIVE_INST_VALU"] / cu_count / (c["GRBM_GUI_ACTIVE"] / 8), 1),
+                   # counter_defs.yaml's VALUBusy formula, 100 * SQ_ACTIVE_INST_VALU
+                   # / CUs / cycles, prices every VALU instruction at 4 cycles
+                   # (SIMD-16) and reads > 100 % on gfx950.  Reported raw (a
+                   # ratio, not a percentage) and scaled to the SIMD-32 issue of
+                   # a full-rate instruction (2 cycles), which cannot exceed 100 %.
+                   "sq_active_inst_valu_per_cu_cycle": round(
+                       c["SQ_ACTIVE_INST_VALU"] / cu_count / (c["GRBM_GUI_ACTIVE"] / 8), 4),
+                   "valu_busy_pct_simd32": round(
+                       50 * c["SQ_ACTIVE_INST_VALU"] / cu_count / (c["GRBM_GUI_ACTIVE"] / 8), 1),
                    "cycles_per_valu_instr": round(4 * cu_count * clock * t_ns * 1e-9 / c["SQ_INSTS_VALU"], 3)}
     return out
 
@@ -505,7 +514,8 @@ def roofline_block(achieved, kms, peak, live, traffic, traffic_source, algo_byte
         if "clock_ghz" in v:
             peak_clk = cu_count * 4 * 32 * v["clock_ghz"] * 1e9 / 1e12
             r["valu_instr_per_hash"] = v["valu_instr_per_hash"]
-            r["valu_busy_pct"] = v["valu_busy_pct"]
+            r["valu_busy_pct_simd32"] = v["valu_busy_pct_simd32"]
+            r["sq_active_inst_valu_per_cu_cycle"] = v["sq_active_inst_valu_per_cu_cycle"]
             r["cycles_per_valu_instr"] = v["cycles_per_valu_instr"]
             r["measured_clock_ghz"] = v["clock_ghz"]
             r["frac_at_measured_clock"] = round(achieved / peak_clk, 4)
@@ -536,6 +546,52 @@ def list_fingerprint(buf, n: int) -> str:
     return hashlib.sha256(a.astype("<u4").tobytes()).hexdigest()
 
 
+def launch_plan(gpus: int, env) -> str:
+    """How this process runs `bench.py --gpus N`:
+      * "run"      — it is one rank already (WORLD_SIZE set by the launcher and
+                     equal to N), or N = 1;
+      * "self"     — N > 1 and no launcher: start torch.distributed.run with N
+                     ranks as a CHILD process (before torch or the GPU is
+                     touched; no exec) and relay its JSON line;
+      * "mismatch" — a launcher started this rank for a job of a different
+                     size than --gpus: measuring it would mislabel n_gpus."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "self" if gpus > 1 else "run"
+    return "run" if int(ws) == gpus else "mismatch"
+
+
+def self_launch(gpus: int, argv: list[str]) -> int:
+    """`python bench.py --gpus N` without a launcher: run the driver's own
+    launch shape (torch.distributed.run, one rank per GPU, rendezvous on
+    127.0.0.1) as a child, pass its JSON line through on stdout (everything
+    else to stderr), and return its exit code."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, cwd=ROOT)
+    for line in p.stdout:
+        if line.startswith("{"):
+            print(line, end="", flush=True)
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+def native_group_error(group, group_err: str | None, world: int, rehearsal: bool) -> str | None:
+    """At N > 1 the per-step collectives and config 4's search must run through
+    the library's own group (RCCL from C++); a job whose pow_group_init failed
+    on any rank stops with this message instead of measuring a fallback."""
+    if world > 1 and not rehearsal and group is None:
+        return group_err or "pow_group_init failed"
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -550,6 +606,13 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
     args = ap.parse_args()
 
+    plan = launch_plan(args.gpus, os.environ)
+    if plan == "self":
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    if plan == "mismatch":
+        print(f"bench.py: --gpus {args.gpus} but the launcher started a job of WORLD_SIZE="
+              f"{os.environ.get('WORLD_SIZE')}", file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -587,8 +650,8 @@ def main():
         try:
             group = RcclGroup.from_torch(miner) if dist is not None else \
                 RcclGroup(miner, 0, 1, RcclGroup.make_unique_id())
-        except Exception as e:  # pragma: no cover - fall back to torch's collectives, say so
-            group_err = f"pow_group_init failed ({e}); torch.distributed collectives used instead"
+        except Exception as e:  # fatal at N > 1 (below); at N = 1 only group_search is lost, said in group_error
+            group_err = f"pow_group_init failed ({e})"
             group = None
         if dist is not None:
             # Every rank uses the native group or none does (a rank that lacks it
@@ -598,7 +661,13 @@ def main():
             if int(ok.item()) == 0 and group is not None:
                 group.close()
                 group = None
-                group_err = "pow_group_init failed on a peer rank; torch.distributed collectives used instead"
+                group_err = "pow_group_init failed on a peer rank"
+        err = native_group_error(group, group_err, world, rehearsal)
+        if err:  # fail loudly: no N > 1 number without the native collectives
+            print(json.dumps({"error": "bench.py: no native pow_group at N > 1", "group_error": err, "rank": rank}),
+                  file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
     info = miner.device_info()
     tmpl = s0_block()
     d = args.difficulty

@@ -59,6 +59,7 @@
 #include <ctime>
 #include <deque>
 #include <fstream>
+#include <iostream>
 #include <map>
 #include <mutex>
 #include <random>
@@ -136,6 +137,36 @@ class Node {
 
   int init_gpu();
   int run();
+#ifdef POW_NODE_TEST_KNOBS
+  // --log-chain-stdin <rank> (test build): no MPI, no GPU.  Load a chain from
+  // stdin (one block per line, tip first: index, owner, previous_block_hash,
+  // block_hash, tab-separated) and write the termination dump exactly as
+  // proof_of_work does (node.cpp:286-289), so tests can compare this node's
+  // log_msg + log_chain with the reference's (oracle/_ref/ref_log_chain).
+  int dump_from_stdin(int rank) {
+    rank_ = rank;
+    std::string line, tip;
+    while (std::getline(std::cin, line)) {
+      std::vector<std::string> f;
+      size_t a = 0;
+      for (size_t t; (t = line.find('\t', a)) != std::string::npos; a = t + 1) f.push_back(line.substr(a, t - a));
+      f.push_back(line.substr(a));
+      if (f.size() != 4 || f[2].size() >= POW_HASH_SIZE || f[3].size() >= POW_HASH_SIZE) continue;
+      pow_block b{};
+      b.index = (uint32_t)std::stoul(f[0]);
+      b.node_owner_number = (uint32_t)std::stoul(f[1]);
+      memcpy(b.previous_block_hash, f[2].data(), f[2].size());
+      memcpy(b.block_hash, f[3].data(), f[3].size());
+      blocks_[f[3]] = b;
+      if (tip.empty()) tip = f[3];
+    }
+    if (tip.empty()) return 2;
+    last_ = &blocks_.at(tip);
+    log_msg("Terminé con la siguiente cadena");
+    log_chain("");
+    return 0;
+  }
+#endif
 
  private:
   // ---- state (node.cpp:19-26) ----
@@ -604,6 +635,9 @@ int Node::run() {
 
 int main(int argc, char** argv) {
   Options o;
+#ifdef POW_NODE_TEST_KNOBS
+  if (argc == 3 && std::string(argv[1]) == "--log-chain-stdin") return Node(o).dump_from_stdin(atoi(argv[2]));
+#endif
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i];
     const long v = strtol(argv[i + 1], nullptr, 10);

@@ -31,6 +31,7 @@ class NetworkRun:
     returncode: int
     stdout: str
     chains: dict = field(default_factory=dict)  # rank -> [ChainEntry] (tip first)
+    dumps: dict = field(default_factory=dict)   # rank -> raw bytes of <rank>.out
 
 
 # A launcher's rank variables (torch.distributed.run sets these in bench.py's
@@ -90,5 +91,7 @@ def run_network(n_gpu: int, workdir: str, difficulty: int = 9, blocks: int = 10,
     for r in range(n_ref + n_gpu):
         f = os.path.join(workdir, f"{r}.out")
         if os.path.exists(f):
-            run.chains[r] = parse_chain_dump(open(f).read())
+            raw = open(f, "rb").read()
+            run.dumps[r] = raw
+            run.chains[r] = parse_chain_dump(raw.decode(errors="replace"))
     return run

@@ -1,5 +1,8 @@
 """Shared helpers for the tests (builds Blocks from golden.json entries)."""
 import ctypes
+import os
+import subprocess
+import tempfile
 
 from mpi_blockchain_amd._lib import Block
 from mpi_blockchain_amd.block import make_block, set_field
@@ -40,3 +43,21 @@ def check_chain(entries, blocks: int, difficulty: int) -> bool:
     for e in entries:
         assert len(e.hash) == 64 and leading_zero_bits(e.hash) >= difficulty
     return idx == list(range(blocks, 0, -1)) and entries[-1].prev == ""
+
+
+REF_LOG_CHAIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                             "ref_log_chain")
+
+
+def reference_dump(entries, rank: int) -> bytes:
+    """The bytes the REFERENCE's log_msg + log_chain (node.cpp:40-68, run as
+    proof_of_work's termination does, node.cpp:286-289) write for this chain
+    (tip first): oracle/_ref/ref_log_chain, built from /root/reference's own
+    node.cpp + block.cpp."""
+    from mpi_blockchain_amd.node import mpi_env
+
+    tsv = "".join(f"{e.index}\t{e.owner}\t{e.prev}\t{e.hash}\n" for e in entries)
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run([REF_LOG_CHAIN, str(rank)], input=tsv.encode(), cwd=td, env=mpi_env(), check=True,
+                       capture_output=True, timeout=60)
+        return open(os.path.join(td, f"{rank}.out"), "rb").read()

@@ -162,3 +162,74 @@ def test_cpu_baseline_headline_is_the_best_run(monkeypatch):
     assert r["value"] >= r["at_cpu_quota"]["value"]
     assert r["logical_cpus"] == 256 and r["physical_cores"] == 128 and r["usable_cpus"] == 16.0
     assert r["as_shipped_O0"] == 5.3e5
+
+
+def test_launch_plan_branches():
+    """--gpus N: no launcher and N > 1 -> launch torch.distributed.run itself;
+    a launcher whose WORLD_SIZE differs from N -> refuse; otherwise run."""
+    assert bench.launch_plan(1, {}) == "run"
+    assert bench.launch_plan(8, {}) == "self"
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}) == "run"
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}) == "run"
+    assert bench.launch_plan(8, {"WORLD_SIZE": "1"}) == "mismatch"
+    assert bench.launch_plan(1, {"WORLD_SIZE": "4"}) == "mismatch"
+
+
+def test_self_launch_runs_torchrun_as_a_child(monkeypatch, capsys):
+    """The self-launch starts torch.distributed.run (one rank per GPU, 127.0.0.1
+    rendezvous) as a child process, relays only its JSON line to stdout and
+    returns the child's exit code."""
+    import io
+
+    seen = {}
+
+    class FakePopen:
+        def __init__(self, cmd, stdout=None, text=None, cwd=None):
+            seen["cmd"] = cmd
+            self.stdout = io.StringIO('[rank0] warming up\n{"metric": "m", "n_gpus": 8}\n[rank3] done\n')
+
+        def wait(self):
+            return 7
+
+    monkeypatch.setattr(bench.subprocess, "Popen", FakePopen)
+    rc = bench.self_launch(8, ["--gpus", "8", "--steps", "3"])
+    cmd = seen["cmd"]
+    assert rc == 7
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and "--nnodes=1" in cmd
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    out = capsys.readouterr()
+    assert out.out == '{"metric": "m", "n_gpus": 8}\n' and "[rank0] warming up" in out.err
+
+
+def test_main_refuses_a_mismatched_launch(monkeypatch):
+    """WORLD_SIZE != --gpus: exit 2 before torch is imported or a GPU is touched."""
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    import pytest
+
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 2
+
+
+def test_main_self_launches_without_a_launcher(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "1"])
+    calls = []
+    monkeypatch.setattr(bench, "self_launch", lambda n, argv: calls.append((n, argv)) or 0)
+    import pytest
+
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and calls == [(4, ["--gpus", "4", "--steps", "1"])]
+
+
+def test_native_group_required_at_n_gt_1():
+    """At N > 1 a failed pow_group_init is fatal (no fallback number); at N = 1
+    and in the one-GPU rehearsal it is not."""
+    assert bench.native_group_error(None, "pow_group_init failed (x)", 8, False) == "pow_group_init failed (x)"
+    assert bench.native_group_error(None, None, 2, False) == "pow_group_init failed"
+    assert bench.native_group_error(object(), None, 8, False) is None
+    assert bench.native_group_error(None, "e", 1, False) is None
+    assert bench.native_group_error(None, "e", 8, True) is None

@@ -1,8 +1,12 @@
 """Protocol runs (BASELINE config 5, scaled to one GPU): MPI networks of
-``pow_node`` ranks mining on the GPU through pow_mine, and mixed networks with
+``pow_node`` ranks mining on the GPU through pow_mine, and a mixed network with
 the REFERENCE's own binary (oracle/_ref/blockchain_ref, built from
 /root/reference) — the reference's picosha2 validation (valid_new_block,
-block.cpp:13-25) accepting GPU-mined blocks is the wire-level parity check.
+block.cpp:13-25) accepting GPU-mined blocks, and pow_node accepting the
+reference's, is the wire-level parity check.  Every
+chain dump a run leaves (<rank>.out) is compared byte for byte with what the
+reference's own log_msg + log_chain (node.cpp:40-68) write for that chain
+(oracle/_ref/ref_log_chain).
 """
 import os
 import re
@@ -10,7 +14,7 @@ import time
 
 import pytest
 
-from helpers import check_chain
+from helpers import REF_LOG_CHAIN, check_chain, reference_dump
 from mpi_blockchain_amd.build import mpi_available
 from mpi_blockchain_amd.node import chain_status, run_network
 
@@ -46,6 +50,7 @@ def test_gpu_network(tmp_path, np_, d):
     complete = [r for r, entries in run.chains.items() if check_chain(entries, 10, d)]
     assert complete, run.stdout[-3000:]
     assert "Agregué un producido" in run.stdout
+    assert_dumps_match_reference(run)
     if d <= 5:
         # every rank mined its own block 1 before anyone published one
         assert len(re.findall(r"Agregué un producido con index 1 ", run.stdout)) == np_, run.stdout[-3000:]
@@ -53,6 +58,54 @@ def test_gpu_network(tmp_path, np_, d):
         # ... and a chain migration (verificar_y_migrar_cadena, node.cpp:152-191)
         # that requested, checked and spliced a peer's branch
         assert MIGRATED.search(run.stdout), run.stdout[-3000:]
+
+
+def assert_dumps_match_reference(run, ranks=None):
+    """Every <rank>.out the run left is byte-identical to the reference's own
+    dump of the same chain (log_msg("Terminé con la siguiente cadena") +
+    log_chain(""), node.cpp:286-289 -> 40-68)."""
+    if not os.path.exists(REF_LOG_CHAIN):
+        pytest.skip("oracle/_ref/ref_log_chain not built")
+    assert run.dumps, run.stdout[-3000:]
+    for r, raw in run.dumps.items():
+        if ranks is None or r in ranks:
+            assert raw == reference_dump(run.chains[r], r), (r, raw[:400])
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference binary not built")
+def test_mixed_with_reference_nodes(tmp_path):
+    """2 reference ranks (the reference's own binary: picosha2 on the CPU) + 2
+    pow_node ranks in one mpiexec at the reference's DEFAULT_DIFFICULTY (9).
+    The reference ranks receive pow_node's MPI_BLOCKs (block.cpp:99-120: 542-B
+    payload, 552-B extent), validate them with picosha2 (valid_new_block,
+    block.cpp:13-25; validate_block_for_chain, node.cpp:194-257) and adopt
+    them; the pow_node ranks validate (K2') and adopt the reference's.  One
+    complete consistent chain; its dump is the reference's format byte for
+    byte."""
+    # --serial-init 1: GPU set-up before MPI_Init, so MPI_Init is every rank's
+    # start line as in the reference (reference ranks join no start barrier).
+    # --idle-below 3 (pow_node_test): the GPU ranks mine only once the chain
+    # holds block 3, so blocks 1-3 come from the reference ranks and both
+    # directions of adoption are certain (with a timing knob alone, a slow box
+    # let the GPU ranks win all 10 blocks in 1 of 2 runs:
+    # profiles/r02/verify/protocol_soak_mixed_*.log).
+    run = run_network(2, str(tmp_path), difficulty=9, blocks=10, timeout=240, ref_binary=REF_BIN, n_ref=2,
+                      extra_args=("--serial-init", "1", "--idle-below", "3"))
+    out = run.stdout
+    assert run.returncode == 0, out[-3000:]
+    assert "Error duro" not in out, out[-3000:]
+    adopted = [(int(r), int(s)) for r, s in
+               re.findall(r"\[(\d)\] Agregado a la lista bloque con index \d+ enviado por (\d)", out)]
+    # reference ranks 0/1 accepted blocks mined by pow_node ranks 2/3 ...
+    assert any(r < 2 <= s for r, s in adopted), out[-3000:]
+    # ... and pow_node ranks accepted blocks mined by the reference
+    assert any(s < 2 <= r for r, s in adopted), out[-3000:]
+    st = {r: chain_status(c, 10, 9) for r, c in run.chains.items()}
+    assert st and all(ok for ok, _ in st.values()) and any(done for _, done in st.values()), (st, out[-3000:])
+    # the chain holds blocks of both kinds of miner
+    owners = {e.owner for c in run.chains.values() for e in c}
+    assert owners & {0, 1} and owners & {2, 3}, owners
+    assert_dumps_match_reference(run)
 
 
 # node.cpp:176: the splice of a checked chain; i >= 0 is the common ancestor's slot
@@ -86,3 +139,4 @@ def test_mutual_chain_request(tmp_path, np_):
     # the rank that completes the chain dumps it and aborts the job (node.cpp:286-290, 330)
     st = [chain_status(c, 10, 9) for c in run.chains.values()]
     assert st and all(ok for ok, _ in st) and any(done for _, done in st), out[-3000:]
+    assert_dumps_match_reference(run)

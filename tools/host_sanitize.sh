@@ -26,7 +26,7 @@ build)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -fPIC -shared -std=c++17 -mcode-object-version=5 \
     -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
     -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer \
-    -I "$R/include" -I "$C" \
+    -DPOW_TEST_HOOKS -I "$R/include" -I "$C" \
     "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
     "$C/valu_peak.hip" -o "$O/libpow_gpu.so"
   $CLANG -std=c11 -O1 -g $SAN -I "$R/include" "$R/examples/mine_chain.c" \
@@ -76,7 +76,7 @@ tsan-build)
   mkdir -p "$T"
   C="$R/mpi_blockchain_amd/csrc"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -fPIC -shared -std=c++17 -mcode-object-version=5 \
-    -Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer -I "$R/include" -I "$C" \
+    -Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer -DPOW_TEST_HOOKS -I "$R/include" -I "$C" \
     "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
     "$C/valu_peak.hip" -o "$T/libpow_gpu.so"
   $CLANGXX -std=c++17 -O1 -g -fsanitize=thread -pthread -DPOW_NODE_TEST_KNOBS -I "$R/include" -I "$MPI_INC" \

@@ -53,7 +53,10 @@ if "GRBM_GUI_ACTIVE" in avg and t:
     per_xcd = avg["GRBM_GUI_ACTIVE"] / 8
     out["clock_ghz"] = per_xcd / t
     if "SQ_ACTIVE_INST_VALU" in avg:
-        out["valu_busy_pct"] = 100 * avg["SQ_ACTIVE_INST_VALU"] / 256 / per_xcd
+        # counter_defs' VALUBusy prices an instruction at 4 cycles (SIMD-16): > 100 % on
+        # gfx950; the raw ratio, and the SIMD-32 scaling (a full-rate instruction = 2 cycles)
+        out["sq_active_inst_valu_per_cu_cycle"] = avg["SQ_ACTIVE_INST_VALU"] / 256 / per_xcd
+        out["valu_busy_pct_simd32"] = 50 * avg["SQ_ACTIVE_INST_VALU"] / 256 / per_xcd
 if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
     fb = avg.get("FETCH_SIZE", 0) * 1024
     wb = avg.get("WRITE_SIZE", 0) * 1024
