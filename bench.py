@@ -277,6 +277,46 @@ def pmc_live(cu_count: int, timeout: float = 120) -> dict:
     return out
 
 
+K2_TOOL = os.path.join(ROOT, "tools", "ab_k2")  # built by __graft_entry__.build()
+
+
+def validation_latency() -> dict:
+    """The validation hash of a received block (valid_new_block,
+    block.cpp:13-25 -> block_to_hash; node.cpp:111-115, 199-253): the call
+    median of pow_hash_block (K2', through the C ABI, tools/ab_k2: 3 x 200
+    calls on 200 blocks) beside the reference's own block_to_hash timed
+    in-process (oracle/_ref, as shipped -O0 and -O2; 2,000 calls)."""
+    import ctypes
+
+    out = {}
+    lib = os.path.join(ROOT, "mpi_blockchain_amd", "libpow_gpu.so")
+    try:
+        p = subprocess.run(["timeout", "-k", "5", "120", K2_TOOL, "3", lib], capture_output=True, text=True,
+                           check=True)
+        g = json.loads(p.stdout.strip().splitlines()[-1])
+        out["pow_hash_block_call_us_median"] = g["call_us_median"]
+        out["pow_hash_block_call_us_p90"] = g["call_us_p90"]
+        out["pow_hash_block_kernel_us_median"] = g["kernel_us_median"]
+        out["calls"] = g["calls"]
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        out["gpu_error"] = str(e)[-300:]
+    try:
+        from oracle.oracle import RefLib, make_oblock
+
+        b = make_oblock(3, 0, 9, 1700000000, b"ab" * 32)
+        for flav in ("O0", "O2"):
+            R = RefLib(flav)
+            R.L.ref_block_to_hash_median_ns.restype = ctypes.c_double
+            R.L.ref_block_to_hash_median_ns.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            out[f"reference_block_to_hash_{flav}_us_median"] = round(
+                R.L.ref_block_to_hash_median_ns(ctypes.byref(b), 2000) / 1e3, 2)
+    except Exception as e:  # pragma: no cover
+        out["reference_error"] = str(e)[-300:]
+    out["note"] = ("one block per call, as validate_block_for_chain checks a received block; GPU: call = "
+                   "launch + kernel + result in mapped host memory; reference: picosha2 + hex on one host core")
+    return out
+
+
 def protocol_runs() -> dict:
     """BASELINE config 1 (the reference: mpiexec -np 4 ./blockchain, 10 blocks
     at DEFAULT_DIFFICULTY = 9, picosha2 on CPU) beside config 5 scaled to this
@@ -833,6 +873,7 @@ def main():
         res["group_error"] = group_err
     if world == 1 and not args.no_protocol:
         res["protocol"] = protocol_runs()
+        res["protocol"]["validation_hash"] = validation_latency()
     if proto is not None:
         res["protocol"] = proto
     buf.free()

@@ -216,6 +216,7 @@ struct pow_ctx {
   bool fault_mine = false;        // every pow_mine[_any] call fails (failure-propagation tests)
   uint64_t lat_max = 1ull << 24;  // first-sub-round cap for K1' (0 = K1 only)
   unsigned lat_wps = 0;           // K1' waves per SIMD at every d (0 = the plan)
+  bool sentinel_idle = false;     // K1 mine launches: the sentinel wave takes no chunk (POW_LAUNCH_SENTINEL_IDLE)
   pow_stats stats{};
 };
 
@@ -295,6 +296,9 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   PowLaunch L;
   int rc = make_launch(start, count, diff, cap, mode, &L);
   if (rc) return rc;
+#ifdef POW_TEST_HOOKS
+  if (ctx->sentinel_idle && mode >= 1) L.mode |= POW_LAUNCH_SENTINEL_IDLE;
+#endif
   if (int rc2 = stage_result(ctx, true, start)) return rc2;
   const unsigned grid = grid_for(ctx, L.n_prefix);
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
@@ -490,6 +494,7 @@ int pow_init(int device, pow_ctx** out) {
   if (const char* fi = getenv("POW_FAULT_INJECT")) ctx->fault_mine = std::strcmp(fi, "mine") == 0;
   if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
   if (const char* lw = getenv("POW_LAT_WPS")) ctx->lat_wps = (unsigned)std::min(8ul, strtoul(lw, nullptr, 0));
+  if (const char* si = getenv("POW_TEST_SENTINEL_IDLE")) ctx->sentinel_idle = si[0] == '1';
   if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
     const int per = atoi(g);
     if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
@@ -652,7 +657,11 @@ int hash_one(pow_ctx* ctx, const pow_block* b, uint8_t* digest, char* hex) {
   PowMsg M;
   uint8_t m[320];
   padded_message(b, m);
-  for (int k = 0; k < 80; ++k) M.w[k] = be32(m + 4 * k);
+  for (int c = 0; c < 5; ++c) {  // the message schedules, K folded in (the rounds run on the GPU)
+    uint32_t w[64];
+    expand(w, m + 64 * c);
+    for (int i = 0; i < 64; ++i) M.kw[c][i] = kK[i] + w[i];
+  }
   if (++ctx->one_seq == 0) ctx->one_seq = 1;  // never 0: the warm-up launch publishes 0
   const uint32_t seq = ctx->one_seq;
   HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, seq));

@@ -101,6 +101,10 @@ __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
 // Chunks 2-4 (K1): the previous chunk's feed-forward H += t and this chunk's
 // first four rounds as one group (rounds4_asm_ff), then 15 groups as above;
 // t ends as this chunk's final state.
+#ifndef POW_TRIM_LAST
+#define POW_TRIM_LAST 0
+#endif
+template <bool LAST = false>
 __device__ __forceinline__ void const_chunk_lds_ff(St& H, St& t, const uint32_t* lkw) {
   POW_SB();
   const uint4 v0 = *reinterpret_cast<const uint4*>(lkw);
@@ -111,7 +115,10 @@ __device__ __forceinline__ void const_chunk_lds_ff(St& H, St& t, const uint32_t*
     POW_SB();
     const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
     POW_SB();
-    rounds4_asm(t, v.x, v.y, v.z, v.w);
+    if (LAST && POW_TRIM_LAST && g == 60)
+      rounds4_asm_last(t, v.x, v.y, v.z, v.w);
+    else
+      rounds4_asm(t, v.x, v.y, v.z, v.w);
   }
   POW_SB();
 }
@@ -271,22 +278,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
   __shared__ uint32_t sibs_done;  // mine modes, workgroup 0: waves 1..3 that have finished (see the exit)
   __shared__ uint32_t wg_tick;                  // dequeue tickets of this workgroup
   __shared__ unsigned long long wg_ring[4];     // (batch + 1) << 32 | base of the batch's first chunk
+  __shared__ uint32_t wg_reads[4];              // reads of the batch that holds each ring slot
   if (threadIdx.x == 0) {
     sibs_done = 0;
     wg_tick = 0;
   }
-  if (threadIdx.x < 4) wg_ring[threadIdx.x] = 0;
+  if (threadIdx.x < 4) {
+    wg_ring[threadIdx.x] = 0;
+    wg_reads[threadIdx.x] = POW_BATCH - 1u;  // as if a batch -4..-1 had been read in full
+  }
   __syncthreads();
 
+  // (test library only: the sentinel idles from the start, pow_template.h)
+  const bool sentinel_idle = MODE >= 1 && (L.mode & POW_LAUNCH_SENTINEL_IDLE) && blockIdx.x == 0 && threadIdx.x < 64u;
   for (;;) {
+    if (sentinel_idle) break;
     // Dequeue one 64-prefix chunk.  Tickets come from an LDS counter: ticket
     // t is chunk t % POW_BATCH of the workgroup's batch t / POW_BATCH, and the
     // wave holding a batch's first ticket claims the whole batch (POW_BATCH
     // chunks) with ONE global atomic and publishes its base in a 4-slot LDS
-    // ring tagged with the batch number; the batch's other waves read it there
-    // (at most 4 waves hold one ticket each, so a slot is not reused while
-    // read).  Chunks are still handed out one per wave in increasing order
-    // within a workgroup, and batches in increasing order across the grid.
+    // ring tagged with the batch number; the batch's other waves read it there.
+    // A slot is reused by batch b + 4 only after all POW_BATCH - 1 readers of
+    // batch b have read it (wg_reads): every drawn ticket is read before its
+    // wave can leave, and batch b's leader published before drawing again, so
+    // the wait ends (without it, a reader stalled while the other
+    // waves drew 25 tickets would have spun forever on an overwritten tag).
+    // Chunks are still handed out one per wave in increasing order within a
+    // workgroup, and batches in increasing order across the grid.
     // 8 chunks per atomic: WRITE_SIZE 73.2 -> 42.7 MB per 2^32 window (the
     // atomics were ~37 MB of it) at equal speed (profiles/r03/ab/ab4_*).
     uint32_t got = 0;
@@ -294,8 +312,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       const uint32_t t = atomicAdd(&wg_tick, 1u);
       const uint32_t b = t / POW_BATCH, slot = t % POW_BATCH;
       unsigned long long* const ring = &wg_ring[b & 3u];
+      uint32_t* const reads = &wg_reads[b & 3u];
       if (slot == 0) {
         got = atomicAdd(&res->next, 64u * POW_BATCH);
+        while (__hip_atomic_load(reads, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != POW_BATCH - 1u)
+          __builtin_amdgcn_s_sleep(1);  // batch b - 4 still has a reader: never in practice
+        __hip_atomic_store(reads, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(ring, ((unsigned long long)(b + 1u) << 32) | got, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
@@ -304,6 +326,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
                b + 1u)
           __builtin_amdgcn_s_sleep(1);
         got = (uint32_t)v + 64u * slot;
+        __hip_atomic_fetch_add(reads, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     const uint32_t rbase = __builtin_amdgcn_readfirstlane(got);
@@ -462,7 +485,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       St t = Hs;
       const_chunk_lds<true>(t, lkw);
 #pragma unroll
-      for (int c = 1; c < 4; ++c) const_chunk_lds_ff(Hs, t, lkw + 64 * c);
+      for (int c = 1; c < 3; ++c) const_chunk_lds_ff(Hs, t, lkw + 64 * c);
+      const_chunk_lds_ff<!FULL>(Hs, t, lkw + 64 * 3);  // d <= 32: only H0 of the last chunk
       // ---------------- chunk 4 (last): only what the test needs ----------------
       const uint32_t h0 = Hs.a + t.a;
 
@@ -763,50 +787,69 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
 // K2': block_to_hash (block.cpp:74-77) of ONE block, for validation
 // (pow_hash_block).  A received block is checked one at a time
 // (validate_block_for_chain, node.cpp:199-253), so the latency of one hash is
-// what counts: one wave, the message by value in the kernarg segment (no H2D
-// copy), the digest and a done word stored into mapped host memory (no D2H
-// copy, no completion-signal wait).  The five chunks' message schedules do not
-// depend on the chaining state, so lanes 0-4 expand them at once (one chunk
-// each, K folded in: K+W into LDS); every lane then runs the 320 rounds
-// (the same values in every lane: no divergence) reading K+W from LDS 4 at a
-// time, and lane 0 publishes.  <= 64 VGPRs: it must fit the workgroup slot a
-// running K1 leaves free.
+// what counts.  One wave; the host expands the five chunks' message schedules
+// (K folded in, as pow_build_consts does for K1's chunks 1-4) and passes the
+// 320 K+W words by value in the kernarg segment, which the wave reads with
+// scalar loads issued ahead of their rounds: no H2D copy, no LDS, no barrier,
+// only the 320 compression rounds (the digest's chained part) on the GPU.  The
+// digest, its duration and a done word go into mapped host memory (no D2H
+// copy, no completion-signal wait).  One wave alone issues a VALU instruction
+// every ~4 cycles whether it is full or half rate (MI355X_MICROARCH.md,
+// vector-instruction issue cost), so the kernel time is the instruction
+// count: 320 rounds x 14 in asm groups with the K+W word in the v_add3 (the
+// compiler's form takes 16: six separate adds), 4,520 in all (round 3's form,
+// which also ran the schedule on the device: 5,100 instructions, 10.9 us).  <= 64 VGPRs: it must fit the
+// workgroup slot a running K1 leaves free.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void pow_hash_one(
     const PowMsg M, PowHashOut* __restrict__ hout, uint32_t seq) {
   (void)M;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   // M is the first kernel argument: read it through the kernarg pointer (its
-  // address would make a private copy).  Lane c < 5 reads its chunk's 16 words.
-  const uint32_t* const msg = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
-  __shared__ __attribute__((aligned(16))) uint32_t kw[5][64];
-  const uint32_t lane = threadIdx.x;
-  if (lane < 5u) {
-    uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = msg[16u * lane + k];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      if (i >= 16) w[i & 15] = ssig1(w[(i + 14) & 15]) + w[(i + 9) & 15] + ssig0(w[(i + 1) & 15]) + w[i & 15];
-      kw[lane][i] = K[i] + w[i & 15];
-    }
-  }
-  __syncthreads();
+  // address would make a private copy); uniform indices -> scalar loads.
+  const uint32_t* const kw = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+#if POW_K2_SMEM
   St h{IV[0], IV[1], IV[2], IV[3], IV[4], IV[5], IV[6], IV[7]};
-#pragma unroll 1
+#pragma unroll
   for (int c = 0; c < 5; ++c) {
     St t = h;
 #pragma unroll
-    for (int g = 0; g < 64; g += 4) {
-      const uint4 v = *reinterpret_cast<const uint4*>(&kw[c][g]);
-      round_k_w(t, v.x, 0u);
-      round_k_w(t, v.y, 0u);
-      round_k_w(t, v.z, 0u);
-      round_k_w(t, v.w, 0u);
+    for (int i = 0; i < 64; i += 4)
+      rounds4_kws_asm_np(t, kw[64 * c + i], kw[64 * c + i + 1], kw[64 * c + i + 2], kw[64 * c + i + 3]);
+#else
+  __shared__ __attribute__((aligned(16))) uint32_t lkw[320];
+  {
+    const uint32_t lane = threadIdx.x;
+    uint32_t v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = kw[lane + 64u * k];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) lkw[lane + 64u * k] = v[k];
+  }
+  __syncthreads();
+  St h{IV[0], IV[1], IV[2], IV[3], IV[4], IV[5], IV[6], IV[7]};
+  // K+W four words at a time, each read issued one group (4 rounds, ~220
+  // cycles) before its use; the waits are explicit (the reads and rounds are
+  // asm, in this order): at group g, wait for read g, issue read g + 1, run g.
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lbase = (uint32_t)(uintptr_t)lkw;
+  u32x4 q;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(q) : "v"(lbase));
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    St t = h;
+#pragma unroll
+    for (int i = 0; i < 64; i += 4) {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(q));  // q holds its words from here on
+      const u32x4 cur = q;
+      if (64 * c + i + 4 < 320)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(q) : "v"(lbase), "i"(4 * (64 * c + i + 4)));
+      rounds4_kwv_asm_v(t, cur.x, cur.y, cur.z, cur.w);
     }
+#endif
     h.a += t.a; h.b += t.b; h.c += t.c; h.d += t.d;
     h.e += t.e; h.f += t.f; h.g += t.g; h.h += t.h;
   }
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     const uint32_t d[8] = {h.a, h.b, h.c, h.d, h.e, h.f, h.g, h.h};
 #pragma unroll
     for (int k = 0; k < 8; ++k) __hip_atomic_store(&hout->digest[k], d[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -112,8 +112,13 @@ struct PowLaunch {
   uint32_t thr;            // d <= 32: solution iff H0 <= thr;  d > 32: thr = 0
   uint32_t diff;           // difficulty in bits
   uint32_t cap;            // sweep output capacity
-  uint32_t mode;           // 0 = sweep (record all), 1 = mine (lowest + early exit)
+  uint32_t mode;           // 0 = sweep (record all), 1 = mine (lowest + early exit); flags below
 };
+// Set only by the test library (POW_TEST_HOOKS): in the mine modes the sentinel
+// wave (workgroup 0, wave 0) takes no chunk and goes straight to its exit wait,
+// so a test can cancel while the sentinel's own work is done and the rest of
+// the grid still runs (the path that keeps cancellation alive in the tail).
+#define POW_LAUNCH_SENTINEL_IDLE 0x100u
 
 // A solution recorded with its digest by the latency kernel, so the winner's
 // block_hash needs no second hashing launch.
@@ -147,10 +152,12 @@ struct PowResult {
   PowHit hit[POW_HITS];
 };
 
-// K2' (pow_hash_block's one-block path): the padded 320-byte message as 80
-// big-endian words, passed by value (kernarg: no H2D copy) ...
+// K2' (pow_hash_block's one-block path): the five chunks' K[i] + W[i] words of
+// the padded 320-byte message (the message schedule, expanded on the host as
+// pow_build_consts does for K1's chunks 1-4), passed by value (kernarg: no H2D
+// copy, read by scalar loads) ...
 struct PowMsg {
-  uint32_t w[80];
+  uint32_t kw[5][64];
 };
 // ... and its result, written by the kernel into mapped host memory (no D2H
 // copy): the digest, the kernel's duration in realtime ticks, and `done` = the

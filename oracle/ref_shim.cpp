@@ -9,11 +9,13 @@
 //
 // Nothing here re-implements the reference: every hash and test below is the
 // reference's own function.
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <string>
+#include <vector>
 
 #include "block.h"  // /root/reference/block.h (via -I)
 
@@ -97,4 +99,24 @@ REF_API uint64_t ref_mine_loop(const Block* last, int rank, uint64_t trials) {
     if (solves_problem(hash_hex_str)) ++hits;
   }
   return hits;
+}
+
+// The validation hash of a received block (valid_new_block, block.cpp:13-25:
+// block_to_hash, block.cpp:74-77), timed in-process: `n` calls on `n` blocks
+// that differ in their nonce; returns the median call time in nanoseconds
+// (bench.py's protocol block, beside pow_hash_block's call median).
+REF_API double ref_block_to_hash_median_ns(const Block* tmpl, int n) {
+  std::vector<double> t((size_t)(n > 0 ? n : 1));
+  Block b = *tmpl;
+  std::string h;
+  for (int i = 0; i < n; ++i) {
+    nonce_from_counter((uint64_t)i * 7919u, b.nonce);
+    timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    block_to_hash(&b, h);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    t[(size_t)i] = (double)(t1.tv_sec - t0.tv_sec) * 1e9 + (double)(t1.tv_nsec - t0.tv_nsec);
+  }
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
 }

@@ -38,7 +38,7 @@ def test_library_exports_all_symbols():
         assert hasattr(L, name), name
 
 
-HOOKS = (b"POW_FAULT_INJECT", b"POW_FORCE_FULL", b"POW_LAT_MAX", b"POW_LAT_WPS", b"POW_GRID_PER_CU",
+HOOKS = (b"POW_FAULT_INJECT", b"POW_FORCE_FULL", b"POW_LAT_MAX", b"POW_LAT_WPS", b"POW_GRID_PER_CU", b"POW_TEST_SENTINEL_IDLE",
          b"POW_TEST_RCCL_LIB")
 
 

@@ -175,3 +175,96 @@ def test_group_mine_any_world1():
             assert r.counter in first21
         # the lowest-counter group search is unchanged by the board
         assert g.mine(b, 0, 1 << 32, 21).counter == FIRST_D21
+
+
+def test_bound_lowest_mode_peer_below_returns_zero():
+    """ADVICE r03 / include/pow_gpu.h: with a bound board, lowest-mode pow_mine
+    returns 0 whenever a peer's slot holds a counter below the one it found,
+    even though its own range holds a solution; the context holding the lower
+    counter returns it.  Two contexts, one board, two searches (tags), both
+    orders: S1's lowest d = 9 solution is 263 and S0's is 238 (golden)."""
+    from mpi_blockchain_amd.miner import GpuMiner, StopBoard
+
+    s1 = make_block(7, 3, 9, 1760572800, b"007384e324711d0c9fab8d3ed9b7be265575e29bde9a9ea56b1d86672ee927e8")
+    with StopBoard(2) as board, GpuMiner(0) as A, GpuMiner(0) as B:
+        for tag in (11, 12):
+            A.bind_board(board, 0, tag)
+            B.bind_board(board, 1, tag)
+            if tag == 11:  # the lower one first: it returns its counter; the higher one then returns 0
+                rb = B.mine(s0(), 0, 1 << 16, 9)
+                ra = A.mine(s1, 0, 1 << 16, 9)
+                assert rb is not None and rb.counter == FIRST_D9
+                assert ra is None
+                # unbound, A's own range does hold a solution
+                A.bind_board(None)
+                assert A.mine(s1, 0, 1 << 16, 9).counter == 263
+            else:  # the higher one first returns 263; the lower one still returns its own 238
+                ra = A.mine(s1, 0, 1 << 16, 9)
+                rb = B.mine(s0(), 0, 1 << 16, 9)
+                assert ra is not None and ra.counter == 263
+                assert rb is not None and rb.counter == FIRST_D9
+                assert board.peek(1, tag) == 263 and board.peek(0, tag) == FIRST_D9
+        A.bind_board(None)
+        B.bind_board(None)
+
+
+def sentinel_idle_miner():
+    """A context of the test library whose K1 mine launches keep the sentinel
+    wave (workgroup 0, wave 0) out of the work queue from the start
+    (POW_TEST_SENTINEL_IDLE), and whose pow_mine skips the latency kernel
+    (POW_LAT_MAX=0), so every launch is K1."""
+    from mpi_blockchain_amd.miner import GpuMiner
+
+    os.environ.update(POW_TEST_SENTINEL_IDLE="1", POW_LAT_MAX="0")
+    try:
+        m = GpuMiner(0, test_hooks=True)
+    finally:
+        del os.environ["POW_TEST_SENTINEL_IDLE"], os.environ["POW_LAT_MAX"]
+    m.warmup()
+    return m
+
+
+@pytest.mark.parametrize("any_solution", [True, False])
+def test_cancel_reaches_the_grid_after_the_sentinel_is_done(any_solution):
+    """the sentinel wave is the only reader of host memory, so it
+    must keep polling after its own chunks are done while the rest of the grid
+    still runs (pow_kernels.hip, the exit wait).  Here it takes no chunk at
+    all (a test-library flag), so every poll of the launch comes from that
+    wait: a cancel 30 ms into a 2^30-counter K1 launch (~0.13 s) must still
+    stop it within a few ms, and a peer's hit on the board likewise.  The
+    same flag leaves the results exact (golden lowest counter)."""
+    from mpi_blockchain_amd.miner import StopBoard
+
+    b = s0()
+    with sentinel_idle_miner() as m:
+        r = m.mine(b, 0, 1 << 26, 21, any_solution=any_solution)
+        assert r is not None and (r.counter == FIRST_D21 or any_solution)
+        m.cancel()  # arm the GPU-side epoch check
+        ep = m.epoch
+        res = {}
+
+        def run():
+            res["r"] = m.mine(b, 0, 1 << 40, 60, epoch=ep, any_solution=any_solution)
+            res["t"] = time.perf_counter()
+
+        th = threading.Thread(target=run)
+        th.start()
+        time.sleep(0.03)
+        t_cancel = time.perf_counter()
+        m.cancel()
+        th.join(timeout=30)
+        assert not th.is_alive() and res["r"] is None
+        assert res["t"] - t_cancel < 0.02, res["t"] - t_cancel
+        # a peer's hit on the board, seen only by the waiting sentinel
+        with StopBoard(2) as board:
+            m.bind_board(board, 0, 21)
+            th = threading.Thread(target=run)
+            ep = m.epoch
+            th.start()
+            time.sleep(0.03)
+            t_post = time.perf_counter()
+            board.post(1, 21, 5)  # below every counter of the range
+            th.join(timeout=30)
+            assert not th.is_alive() and res["r"] is None
+            assert res["t"] - t_post < 0.02, res["t"] - t_post
+            m.bind_board(None)

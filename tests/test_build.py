@@ -266,3 +266,15 @@ def test_latency_kernel_asm_variant(isa, variant):
     body = j_loop_body(isa, variant)
     assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 64
     assert body.count(".p2align 3") == 64
+
+
+def test_k2_one_block_is_the_rounds_only(isa):
+    """K2' (round 4): the host expands the message schedules (K folded in), so
+    the kernel is the 320 compression rounds of one block, 14 VALU each in asm
+    groups (the compiler's form takes 16), plus the feed-forward: ~4,565 VALU
+    (round 3: ~5,100 with the schedules on the device).  Its 80 K+W reads
+    (ds_read_b128) are each issued one group ahead of their use."""
+    body = kernel_body(isa, "_Z12pow_hash_one")
+    assert 4480 <= len(re.findall(r"^\s+v_", body, flags=re.M)) <= 4620
+    assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 80
+    assert len(re.findall(r"^\s+v_add3_u32", body, flags=re.M)) == 2 * 320
