@@ -41,6 +41,9 @@ def test_bench_json_contract():
     assert 4700 < r["valu_instr_per_hash"] < 5000, live
     assert 1.5 < r["measured_clock_ghz"] < 2.5 and 2.0 <= r["cycles_per_valu_instr"] < 6, live
     assert 0 < r["issued_frac_at_measured_clock"] <= r["frac_at_measured_clock"] < 1.0, r
+    # no figure labelled "busy" above 100 % (counter_defs' VALUBusy prices SIMD-16 issue)
+    assert 0 < r["valu_busy_pct_simd32"] <= 100, r
+    assert not [k for k, v in r.items() if "busy" in k and isinstance(v, (int, float)) and v > 100], r
 
 
 def test_valu_microbench_ceilings():
