@@ -98,6 +98,43 @@ __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
   }
 }
 
+// K1' at 1-2 waves per SIMD (round 4): chunks 1-4 as 14-op asm groups (no
+// phase pin: at one wave per SIMD every VALU instruction issues ~4 cycles
+// apart whatever its rate) whose K+W reads are issued one group (~56
+// instructions) ahead of their use and waited for explicitly; the compiler's
+// schedule issued each read ~10 instructions ahead, and one wave per SIMD has
+// no other wave to cover the LDS latency.  H holds chunk 1's input state;
+// afterwards H holds chunk 4's input state and t chunk 4's final state.
+#ifndef POW_LAT_PIPE
+#define POW_LAT_PIPE 1
+#endif
+// K2' (one block, one wave) runs its 5 chunks through the same helper (NC = 5).
+template <int NC = 4>
+__device__ __forceinline__ void const_chunks_lds_pipelined(uint32_t H[8], St& t, const uint32_t* lk) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lbase = (uint32_t)(uintptr_t)lk;
+  u32x4 q;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(q) : "v"(lbase));
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int g = 0; g < 64; g += 4) {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(q));  // q holds its words from here on
+      const u32x4 cur = q;
+      if (64 * c + g + 4 < 64 * NC)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(q) : "v"(lbase), "i"(4 * (64 * c + g + 4)));
+      if (g == 0)
+        t = rounds4_asm_from_v(St{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]}, cur.x, cur.y, cur.z, cur.w);
+      else
+        rounds4_kwv_asm_v(t, cur.x, cur.y, cur.z, cur.w);
+    }
+    if (c < NC - 1) {
+      H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
+      H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
+    }
+  }
+}
+
 // Chunks 2-4 (K1): the previous chunk's feed-forward H += t and this chunk's
 // first four rounds as one group (rounds4_asm_ff), then 15 groups as above;
 // t ends as this chunk's final state.
@@ -681,15 +718,20 @@ __global__ __launch_bounds__(256) void pow_search_lat(
     uint32_t lo = 0;
     asm volatile("" : "+v"(lo) : "v"(s.a));
     const uint32_t* lk = lkw + lo;
+    St t;
+    if (!ASM && POW_LAT_PIPE) {
+      const_chunks_lds_pipelined(H, t, lk);
+    } else {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-      const_chunk_lds<ASM>(t, lk + 64 * c);
-      H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
-      H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
+      for (int c = 0; c < 3; ++c) {
+        t = St{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+        const_chunk_lds<ASM>(t, lk + 64 * c);
+        H[0] += t.a; H[1] += t.b; H[2] += t.c; H[3] += t.d;
+        H[4] += t.e; H[5] += t.f; H[6] += t.g; H[7] += t.h;
+      }
+      t = St{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
+      const_chunk_lds<ASM>(t, lk + 64 * 3);
     }
-    St t{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
-    const_chunk_lds<ASM>(t, lk + 64 * 3);
     // The whole digest stays live here (this kernel runs at <= 4 waves/SIMD,
     // so the 7 extra VGPRs cost no residency): a hit records it, and the
     // winner's block_hash needs no K2 launch (one serial SHA-256 of 5 chunks
@@ -815,6 +857,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
 #pragma unroll
     for (int i = 0; i < 64; i += 4)
       rounds4_kws_asm_np(t, kw[64 * c + i], kw[64 * c + i + 1], kw[64 * c + i + 2], kw[64 * c + i + 3]);
+    h.a += t.a; h.b += t.b; h.c += t.c; h.d += t.d;
+    h.e += t.e; h.f += t.f; h.g += t.g; h.h += t.h;
+  }
 #else
   __shared__ __attribute__((aligned(16))) uint32_t lkw[320];
   {
@@ -826,29 +871,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
     for (int k = 0; k < 5; ++k) lkw[lane + 64u * k] = v[k];
   }
   __syncthreads();
-  St h{IV[0], IV[1], IV[2], IV[3], IV[4], IV[5], IV[6], IV[7]};
   // K+W four words at a time, each read issued one group (4 rounds, ~220
-  // cycles) before its use; the waits are explicit (the reads and rounds are
-  // asm, in this order): at group g, wait for read g, issue read g + 1, run g.
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const uint32_t lbase = (uint32_t)(uintptr_t)lkw;
-  u32x4 q;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(q) : "v"(lbase));
-#pragma unroll
-  for (int c = 0; c < 5; ++c) {
-    St t = h;
-#pragma unroll
-    for (int i = 0; i < 64; i += 4) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(q));  // q holds its words from here on
-      const u32x4 cur = q;
-      if (64 * c + i + 4 < 320)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(q) : "v"(lbase), "i"(4 * (64 * c + i + 4)));
-      rounds4_kwv_asm_v(t, cur.x, cur.y, cur.z, cur.w);
-    }
+  // cycles) before its use (const_chunks_lds_pipelined, as K1' at one wave
+  // per SIMD); the first group of each chunk leaves the chunk's input state
+  // untouched for the feed-forward.
+  uint32_t H[8] = {IV[0], IV[1], IV[2], IV[3], IV[4], IV[5], IV[6], IV[7]};
+  St t;
+  const_chunks_lds_pipelined<5>(H, t, lkw);
+  const St h{H[0] + t.a, H[1] + t.b, H[2] + t.c, H[3] + t.d, H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
 #endif
-    h.a += t.a; h.b += t.b; h.c += t.c; h.d += t.d;
-    h.e += t.e; h.f += t.f; h.g += t.g; h.h += t.h;
-  }
   if (threadIdx.x == 0) {
     const uint32_t d[8] = {h.a, h.b, h.c, h.d, h.e, h.f, h.g, h.h};
 #pragma unroll

@@ -201,6 +201,21 @@ __device__ __forceinline__ void rounds4_kwv_asm_v(St& s, uint32_t k0, uint32_t k
                : [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
   s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
 }
+// ... and the first group of a chunk reading the chunk's input state without
+// modifying it (the feed-forward needs it): no copies at the chunk boundary.
+__device__ __forceinline__ St rounds4_asm_from_v(const St& in, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
+  St o;
+  asm volatile(POW_RX("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[od]", "%[oh]", "%[k0]")
+               POW_RX("%[oh]", "%[a]", "%[b]", "%[c]", "%[od]", "%[e]", "%[f]", "%[g]", "%[oc]", "%[og]", "%[k1]")
+               POW_RX("%[og]", "%[oh]", "%[a]", "%[b]", "%[oc]", "%[od]", "%[e]", "%[f]", "%[ob]", "%[of]", "%[k2]")
+               POW_RX("%[of]", "%[og]", "%[oh]", "%[a]", "%[ob]", "%[oc]", "%[od]", "%[e]", "%[oa]", "%[oe]", "%[k3]")
+               : [oa] "=&v"(o.a), [ob] "=&v"(o.b), [oc] "=&v"(o.c), [od] "=&v"(o.d), [oe] "=&v"(o.e),
+                 [of] "=&v"(o.f), [og] "=&v"(o.g), [oh] "=&v"(o.h), POW_TEMPS
+               : [a] "v"(in.a), [b] "v"(in.b), [c] "v"(in.c), [d] "v"(in.d), [e] "v"(in.e), [f] "v"(in.f),
+                 [g] "v"(in.g), [h] "v"(in.h), [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
+  return St{o.e, o.f, o.g, o.h, o.a, o.b, o.c, o.d};
+}
 // Four chunk-0 rounds with uniform K+W words (SGPR operands).
 __device__ __forceinline__ void rounds4_kws_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
