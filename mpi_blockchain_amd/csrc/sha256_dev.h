@@ -179,6 +179,34 @@ __device__ __forceinline__ void rounds4_kws_asm_np(St& s, uint32_t k0, uint32_t 
                : [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3));
   s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
 }
+// One-wave issue order (K2', and K1' at 1-2 waves per SIMD, round 4): with no
+// other wave to issue between them, an instruction right after the one it
+// depends on waits for its result, so the 14 ops of a round are spread to
+// keep every operand at least two instructions old: the e rotations, Ch, then
+// the a rotations interleaved with S1, h + K+W and T1, then Maj, S0, e', a'.
+// (The 8-wave order above groups the e-path first: other waves fill the gaps.)
+#ifndef POW_1W_ORDER
+#define POW_1W_ORDER 1
+#endif
+#if POW_1W_ORDER
+#define POW_RX_1W(a, b, c, d, e, f, g, h, dd, hh, KW)                  \
+  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                           \
+  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                          \
+  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                          \
+  "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"             \
+  "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                           \
+  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"             \
+  "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                          \
+  "\tv_add_u32_e64 " hh ", " h ", " KW "\n"                             \
+  "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                          \
+  "\tv_add3_u32 " hh ", " hh ", %[t5], %[t0]\n"                         \
+  "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"             \
+  "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"             \
+  "\tv_add_u32_e64 " dd ", " d ", " hh "\n"                             \
+  "\tv_add3_u32 " hh ", " hh ", %[t2], %[t1]\n"
+#else
+#define POW_RX_1W POW_RX
+#endif
 // ... and with the K+W words in VGPRs (read from LDS).
 __device__ __forceinline__ void rounds4_kwv_asm_np(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
@@ -193,10 +221,10 @@ __device__ __forceinline__ void rounds4_kwv_asm_np(St& s, uint32_t k0, uint32_t 
 // ... volatile: ordered with K2''s explicit LDS reads and waits.
 __device__ __forceinline__ void rounds4_kwv_asm_v(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
-  asm volatile(POW_R_KWS("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]")
-               POW_R_KWS("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]")
-               POW_R_KWS("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]")
-               POW_R_KWS("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]")
+  asm volatile(POW_RX_1W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[d]", "%[h]", "%[k0]")
+               POW_RX_1W("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[c]", "%[g]", "%[k1]")
+               POW_RX_1W("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[b]", "%[f]", "%[k2]")
+               POW_RX_1W("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[a]", "%[e]", "%[k3]")
                : POW_STATE_OPS, POW_TEMPS
                : [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
   s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
@@ -206,10 +234,10 @@ __device__ __forceinline__ void rounds4_kwv_asm_v(St& s, uint32_t k0, uint32_t k
 __device__ __forceinline__ St rounds4_asm_from_v(const St& in, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
   St o;
-  asm volatile(POW_RX("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[od]", "%[oh]", "%[k0]")
-               POW_RX("%[oh]", "%[a]", "%[b]", "%[c]", "%[od]", "%[e]", "%[f]", "%[g]", "%[oc]", "%[og]", "%[k1]")
-               POW_RX("%[og]", "%[oh]", "%[a]", "%[b]", "%[oc]", "%[od]", "%[e]", "%[f]", "%[ob]", "%[of]", "%[k2]")
-               POW_RX("%[of]", "%[og]", "%[oh]", "%[a]", "%[ob]", "%[oc]", "%[od]", "%[e]", "%[oa]", "%[oe]", "%[k3]")
+  asm volatile(POW_RX_1W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[od]", "%[oh]", "%[k0]")
+               POW_RX_1W("%[oh]", "%[a]", "%[b]", "%[c]", "%[od]", "%[e]", "%[f]", "%[g]", "%[oc]", "%[og]", "%[k1]")
+               POW_RX_1W("%[og]", "%[oh]", "%[a]", "%[b]", "%[oc]", "%[od]", "%[e]", "%[f]", "%[ob]", "%[of]", "%[k2]")
+               POW_RX_1W("%[of]", "%[og]", "%[oh]", "%[a]", "%[ob]", "%[oc]", "%[od]", "%[e]", "%[oa]", "%[oe]", "%[k3]")
                : [oa] "=&v"(o.a), [ob] "=&v"(o.b), [oc] "=&v"(o.c), [od] "=&v"(o.d), [oe] "=&v"(o.e),
                  [of] "=&v"(o.f), [og] "=&v"(o.g), [oh] "=&v"(o.h), POW_TEMPS
                : [a] "v"(in.a), [b] "v"(in.b), [c] "v"(in.c), [d] "v"(in.d), [e] "v"(in.e), [f] "v"(in.f),

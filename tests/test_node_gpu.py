@@ -60,16 +60,24 @@ def test_gpu_network(tmp_path, np_, d):
         assert MIGRATED.search(run.stdout), run.stdout[-3000:]
 
 
-def assert_dumps_match_reference(run, ranks=None):
-    """Every <rank>.out the run left is byte-identical to the reference's own
-    dump of the same chain (log_msg("Terminé con la siguiente cadena") +
-    log_chain(""), node.cpp:286-289 -> 40-68)."""
+def assert_dumps_match_reference(run):
+    """Every complete chain dump (<rank>.out) the run left is byte-identical to
+    the reference's own dump of the same chain (log_msg("Terminé con la
+    siguiente cadena") + log_chain(""), node.cpp:286-289 -> 40-68).  A rank
+    that reached the end too but was killed by the first finisher's MPI_Abort
+    (node.cpp:330) while writing leaves a cut dump: it must be a byte prefix of
+    a complete one's reference dump."""
     if not os.path.exists(REF_LOG_CHAIN):
         pytest.skip("oracle/_ref/ref_log_chain not built")
-    assert run.dumps, run.stdout[-3000:]
+    refs = {}
     for r, raw in run.dumps.items():
-        if ranks is None or r in ranks:
-            assert raw == reference_dump(run.chains[r], r), (r, raw[:400])
+        if chain_status(run.chains[r], 10, 0)[1]:
+            refs[r] = reference_dump(run.chains[r], r)
+            assert raw == refs[r], (r, raw[:400])
+    assert refs, run.stdout[-3000:]
+    for r, raw in run.dumps.items():
+        if r not in refs:
+            assert any(ref.startswith(raw) for ref in refs.values()), (r, raw[:400])
 
 
 @pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference binary not built")

@@ -191,7 +191,8 @@ def test_group_multiprocess(world, transport):
     if transport == "rccl_stub":
         for r in range(world):
             assert out[r]["shm_left"] == [], out[r]["shm_left"]
-            assert out[r]["stub_allreduces"] >= 10, out[r]["stub_allreduces"]
+            # every one of the 7 group searches above ends its rounds with the stand-in's all-reduce
+            assert out[r]["stub_allreduces"] >= 7, out[r]["stub_allreduces"]
     for key, ctr, d in (("d21", 2392323, 21), ("d25", 73523910, 25), ("d13_rounds", 6399, 13)):
         vals = {out[r][key][:3] for r in range(world)}
         assert len(vals) == 1, (key, vals)  # the same result on every rank
