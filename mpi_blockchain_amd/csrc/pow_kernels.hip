@@ -98,15 +98,19 @@ __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
   }
 }
 
-// K1' at 1-2 waves per SIMD (round 4): chunks 1-4 as 14-op asm groups (no
-// phase pin: at one wave per SIMD every VALU instruction issues ~4 cycles
-// apart whatever its rate) whose K+W reads are issued one group (~56
-// instructions) ahead of their use and waited for explicitly; the compiler's
-// schedule issued each read ~10 instructions ahead, and one wave per SIMD has
-// no other wave to cover the LDS latency.  H holds chunk 1's input state;
-// afterwards H holds chunk 4's input state and t chunk 4's final state.
+// Chunks as 14-op asm groups in the one-wave order (sha256_dev.h POW_RX_1W)
+// whose K+W reads are issued one group (~56 instructions) ahead of their use
+// and waited for explicitly; the first group of each chunk leaves the chunk's
+// input state untouched for the feed-forward.  H holds the first chunk's
+// input state; afterwards H holds the last chunk's input state and t its
+// final state.  Used by K2' (5 chunks, one wave: kernel 10.9 -> 10.0 us with
+// the host-side schedule, profiles/r04/ab/ab1_*, ab2_*).  For K1' at 1-2 waves
+// per SIMD (chunks 1-4, POW_LAT_PIPE=1) it measured no better than the
+// compiler's rounds, whose reads sit ~10 instructions ahead: time-to-block
+// d = 9 0.0237 -> 0.0243 ms, d = 13 0.0334 -> 0.0340, d = 17 0.0473 -> 0.0471
+// (profiles/r04/ab/ab4_*), so K1' keeps the compiler's form.
 #ifndef POW_LAT_PIPE
-#define POW_LAT_PIPE 1
+#define POW_LAT_PIPE 0
 #endif
 // K2' (one block, one wave) runs its 5 chunks through the same helper (NC = 5).
 template <int NC = 4>
@@ -138,10 +142,6 @@ __device__ __forceinline__ void const_chunks_lds_pipelined(uint32_t H[8], St& t,
 // Chunks 2-4 (K1): the previous chunk's feed-forward H += t and this chunk's
 // first four rounds as one group (rounds4_asm_ff), then 15 groups as above;
 // t ends as this chunk's final state.
-#ifndef POW_TRIM_LAST
-#define POW_TRIM_LAST 0
-#endif
-template <bool LAST = false>
 __device__ __forceinline__ void const_chunk_lds_ff(St& H, St& t, const uint32_t* lkw) {
   POW_SB();
   const uint4 v0 = *reinterpret_cast<const uint4*>(lkw);
@@ -152,10 +152,7 @@ __device__ __forceinline__ void const_chunk_lds_ff(St& H, St& t, const uint32_t*
     POW_SB();
     const uint4 v = *reinterpret_cast<const uint4*>(lkw + g);
     POW_SB();
-    if (LAST && POW_TRIM_LAST && g == 60)
-      rounds4_asm_last(t, v.x, v.y, v.z, v.w);
-    else
-      rounds4_asm(t, v.x, v.y, v.z, v.w);
+    rounds4_asm(t, v.x, v.y, v.z, v.w);
   }
   POW_SB();
 }
@@ -521,9 +518,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
       St Hs{H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7]};
       St t = Hs;
       const_chunk_lds<true>(t, lkw);
+      // (chunk 4's last round still computes e' although H0 needs only a':
+      // skipping it measured 469.40 vs 469.36 ms per window, profiles/r04/ab/ab5_*)
 #pragma unroll
-      for (int c = 1; c < 3; ++c) const_chunk_lds_ff(Hs, t, lkw + 64 * c);
-      const_chunk_lds_ff<!FULL>(Hs, t, lkw + 64 * 3);  // d <= 32: only H0 of the last chunk
+      for (int c = 1; c < 4; ++c) const_chunk_lds_ff(Hs, t, lkw + 64 * c);
       // ---------------- chunk 4 (last): only what the test needs ----------------
       const uint32_t h0 = Hs.a + t.a;
 
@@ -849,18 +847,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
   // M is the first kernel argument: read it through the kernarg pointer (its
   // address would make a private copy); uniform indices -> scalar loads.
   const uint32_t* const kw = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
-#if POW_K2_SMEM
-  St h{IV[0], IV[1], IV[2], IV[3], IV[4], IV[5], IV[6], IV[7]};
-#pragma unroll
-  for (int c = 0; c < 5; ++c) {
-    St t = h;
-#pragma unroll
-    for (int i = 0; i < 64; i += 4)
-      rounds4_kws_asm_np(t, kw[64 * c + i], kw[64 * c + i + 1], kw[64 * c + i + 2], kw[64 * c + i + 3]);
-    h.a += t.a; h.b += t.b; h.c += t.c; h.d += t.d;
-    h.e += t.e; h.f += t.f; h.g += t.g; h.h += t.h;
-  }
-#else
   __shared__ __attribute__((aligned(16))) uint32_t lkw[320];
   {
     const uint32_t lane = threadIdx.x;
@@ -879,7 +865,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
   St t;
   const_chunks_lds_pipelined<5>(H, t, lkw);
   const St h{H[0] + t.a, H[1] + t.b, H[2] + t.c, H[3] + t.d, H[4] + t.e, H[5] + t.f, H[6] + t.g, H[7] + t.h};
-#endif
   if (threadIdx.x == 0) {
     const uint32_t d[8] = {h.a, h.b, h.c, h.d, h.e, h.f, h.g, h.h};
 #pragma unroll

@@ -164,21 +164,6 @@ __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { rou
 #define POW_STATE_OPS                                                                             \
   [a] "+v"(s.a), [b] "+v"(s.b), [c] "+v"(s.c), [d] "+v"(s.d), [e] "+v"(s.e), [f] "+v"(s.f),        \
       [g] "+v"(s.g), [h] "+v"(s.h)
-// The same four rounds without the code-phase pin, for K2' (one wave: every
-// VALU instruction issues ~4 cycles apart whatever its rate or phase, so only
-// the count matters: 14 per round with the K+W word in the v_add3).
-// Not volatile: the compiler may hoist the scalar loads of later K+W words
-// above earlier groups (the groups are pure functions of their operands).
-__device__ __forceinline__ void rounds4_kws_asm_np(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
-  asm(POW_R_KWS("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]")
-               POW_R_KWS("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]")
-               POW_R_KWS("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]")
-               POW_R_KWS("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]")
-               : POW_STATE_OPS, POW_TEMPS
-               : [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3));
-  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
-}
 // One-wave issue order (K2', and K1' at 1-2 waves per SIMD, round 4): with no
 // other wave to issue between them, an instruction right after the one it
 // depends on waits for its result, so the 14 ops of a round are spread to
@@ -207,18 +192,8 @@ __device__ __forceinline__ void rounds4_kws_asm_np(St& s, uint32_t k0, uint32_t 
 #else
 #define POW_RX_1W POW_RX
 #endif
-// ... and with the K+W words in VGPRs (read from LDS).
-__device__ __forceinline__ void rounds4_kwv_asm_np(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
-  asm(POW_R_KWS("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]")
-      POW_R_KWS("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]")
-      POW_R_KWS("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]")
-      POW_R_KWS("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]")
-      : POW_STATE_OPS, POW_TEMPS
-      : [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
-  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
-}
-// ... volatile: ordered with K2''s explicit LDS reads and waits.
+// Four rounds in the one-wave order, K+W in VGPRs (from LDS), in place;
+// volatile: ordered with the explicit LDS reads and waits around them.
 __device__ __forceinline__ void rounds4_kwv_asm_v(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
   asm volatile(POW_RX_1W("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[d]", "%[h]", "%[k0]")
@@ -419,35 +394,6 @@ __device__ __forceinline__ void rounds4_w_asm(St& s, uint32_t k0, uint32_t k1, u
 }
 
 // In place: the state is read and written in the same registers.
-// The last four rounds of the last chunk when only H0 is tested (d <= 32):
-// round 63's e' (d + T1) feeds nothing H0 needs, so it is not computed
-// (13 VALU in that round).  s.e..s.h hold garbage afterwards.
-#define POW_R_LAST(a, b, c, d, e, f, g, h, KW)                          \
-  "\tv_alignbit_b32 %[t5], " e ", " e ", 6\n"                           \
-  "\tv_bitop3_b32 %[t0], " e ", " f ", " g " bitop3:0xca\n"             \
-  "\tv_bitop3_b32 %[t1], " a ", " b ", " c " bitop3:0xe8\n"             \
-  "\tv_alignbit_b32 %[t6], " e ", " e ", 11\n"                          \
-  "\tv_add_u32_e64 " h ", " h ", " KW "\n"                             \
-  "\tv_alignbit_b32 %[t7], " e ", " e ", 25\n"                          \
-  "\tv_bitop3_b32 %[t5], %[t5], %[t6], %[t7] bitop3:0x96\n"             \
-  "\tv_add3_u32 " h ", " h ", %[t5], %[t0]\n"                         \
-  "\tv_alignbit_b32 %[t2], " a ", " a ", 2\n"                           \
-  "\tv_alignbit_b32 %[t3], " a ", " a ", 13\n"                          \
-  "\tv_alignbit_b32 %[t4], " a ", " a ", 22\n"                          \
-  "\tv_bitop3_b32 %[t2], %[t2], %[t3], %[t4] bitop3:0x96\n"             \
-  "\tv_add3_u32 " h ", " h ", %[t2], %[t1]\n"
-__device__ __forceinline__ void rounds4_asm_last(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
-  asm volatile(POW_PHASE
-               POW_R("%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[h]", "%[k0]")
-               POW_R("%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[g]", "%[k1]")
-               POW_R("%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[f]", "%[k2]")
-               POW_R_LAST("%[f]", "%[g]", "%[h]", "%[a]", "%[b]", "%[c]", "%[d]", "%[e]", "%[k3]")
-               : [a] "+v"(s.a), [b] "+v"(s.b), [c] "+v"(s.c), [d] "+v"(s.d), [e] "+v"(s.e), [f] "+v"(s.f),
-                 [g] "+v"(s.g), [h] "+v"(s.h), POW_TEMPS
-               : [k0] "v"(k0), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3));
-  s = St{s.e, s.f, s.g, s.h, s.a, s.b, s.c, s.d};
-}
 __device__ __forceinline__ void rounds4_asm(St& s, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7;
   asm volatile(POW_PHASE
