@@ -164,12 +164,14 @@ __device__ __forceinline__ void round_k_w_o(St& s, uint32_t k, uint32_t w) { rou
 #define POW_STATE_OPS                                                                             \
   [a] "+v"(s.a), [b] "+v"(s.b), [c] "+v"(s.c), [d] "+v"(s.d), [e] "+v"(s.e), [f] "+v"(s.f),        \
       [g] "+v"(s.g), [h] "+v"(s.h)
-// One-wave issue order (K2', and K1' at 1-2 waves per SIMD, round 4): with no
-// other wave to issue between them, an instruction right after the one it
-// depends on waits for its result, so the 14 ops of a round are spread to
-// keep every operand at least two instructions old: the e rotations, Ch, then
-// the a rotations interleaved with S1, h + K+W and T1, then Maj, S0, e', a'.
-// (The 8-wave order above groups the e-path first: other waves fill the gaps.)
+// One-wave issue order (K2', round 4): with no other wave to issue between
+// them, an instruction right after the one it depends on waits for its
+// result, so the 14 ops of a round are spread to keep every operand at least
+// two instructions old: the e rotations, Ch, then the a rotations interleaved
+// with S1, h + K+W and T1, then Maj, S0, e', a'.  (The 8-wave order above
+// groups the e-path first: other waves fill the gaps.)  K2' kernel 10.12 ->
+// 10.04 us against the 8-wave order (profiles/r04/ab/ab2_*): one wave issues
+// ~5 cycles per instruction either way, so the count, not the order, sets it.
 #ifndef POW_1W_ORDER
 #define POW_1W_ORDER 1
 #endif
