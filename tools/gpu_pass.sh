@@ -1,0 +1,49 @@
+#!/bin/bash
+# One GPU pass made of named steps, each under its own time limit (tools/gpu_step.sh);
+# a fault, abort or timeout in one step ends the pass.  Run on the GPU box:
+#   /usr/local/graft/bin/gpurun -- 'bash tools/gpu_pass.sh tests bench profile'
+#
+# steps:
+#   tests            the whole GPU suite (pytest -m gpu)
+#   smoke            __graft_entry__.smoke()
+#   bench            python bench.py (default: N = 1, every block of the JSON line)
+#   profile          tools/profile_round.sh r04 (kernel trace + 4 PMC passes of the bench workload)
+#   fuzz             randomised parity, shipped library: 1,000 cases (tests/parity_fuzz.py)
+#   ab_k1 L...       K1 sweep A/B over libpow_gpu.so builds (tools/ab_sweep, 9 alternating windows)
+#   ab_k2 L...       pow_hash_block A/B (tools/ab_k2, 5 x 200 calls)
+#   ttb D L...       time-to-block A/B at difficulty D (tools/ab_ttb, 301 templates)
+#   k2_trace         rocprofv3 HIP API + kernel trace of 200 pow_hash_block calls
+#   pmc_onewave      PMC (clock, wave cycles, VALU) of K2' and of K1' at d = 9
+# A/B library lists end at the next step name.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+S="$R/tools/gpu_step.sh"
+L="$R/mpi_blockchain_amd/libpow_gpu.so"
+STEPS=" tests smoke bench profile fuzz ab_k1 ab_k2 ttb k2_trace pmc_onewave "
+libs() {  # the library arguments of an A/B step
+  LIBS=()
+  while [ $# -gt 0 ] && [[ "$STEPS" != *" $1 "* ]]; do LIBS+=("$1"); shift; done
+}
+cd "$R"
+while [ $# -gt 0 ]; do
+  step=$1; shift
+  case "$step" in
+    tests) $S gputests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread || exit $? ;;
+    smoke) $S smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) $S bench 900 python -u bench.py || exit $? ;;
+    profile) bash "$R/tools/profile_round.sh" r04 || exit $? ;;
+    fuzz) $S fuzz 900 python -u tests/parity_fuzz.py --cases 1000 --seed 404 || exit $? ;;
+    ab_k1) libs "$@"; shift ${#LIBS[@]}; $S ab_k1 400 tools/ab_sweep 9 "${LIBS[@]}" || exit $? ;;
+    ab_k2) libs "$@"; shift ${#LIBS[@]}; $S ab_k2 200 tools/ab_k2 5 "${LIBS[@]}" || exit $? ;;
+    ttb) d=$1; shift; libs "$@"; shift ${#LIBS[@]}; $S ttb_d$d 300 tools/ab_ttb "$d" 301 "${LIBS[@]}" || exit $? ;;
+    k2_trace) (cd /tmp && export TMPDIR=/tmp && $S k2_trace 120 rocprofv3 --kernel-trace --hip-trace --stats -f csv \
+                 -d "$R/gpurun_out/k2_trace" -o run -- "$R/tools/ab_k2" 1 "$L") || exit $? ;;
+    pmc_onewave) (cd /tmp && export TMPDIR=/tmp &&
+        $S k2_pmc 90 timeout -s KILL 60 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES \
+          --kernel-trace -f csv --kernel-include-regex pow_hash_one -d "$R/gpurun_out/k2_pmc" -o run -- "$R/tools/ab_k2" 1 "$L" &&
+        $S lat_pmc 90 timeout -s KILL 60 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES \
+          --kernel-trace -f csv --kernel-include-regex pow_search_lat -d "$R/gpurun_out/lat_pmc" -o run -- "$R/tools/ab_ttb" 9 101 "$L") \
+        || exit $? ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
