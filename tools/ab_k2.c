@@ -58,6 +58,12 @@ int main(int argc, char** argv) {
     hash[l] = (hash_fn)dlsym(h, "pow_hash_block");
     stats[l] = (stats_fn)dlsym(h, "pow_get_stats");
     if (init(0, &ctx[l]) || warm(ctx[l])) return 1;
+    /* AB_K2_IDLE_CTX=n: n more contexts of this library that never hash (their streams exist) */
+    const char* e = getenv("AB_K2_IDLE_CTX");
+    for (int k = 0; e && k < atoi(e); ++k) {
+      pow_ctx* idle;
+      if (init(0, &idle) || warm(idle)) return 1;
+    }
   }
   static double call[MAXL][4096], kern[MAXL][4096];
   static char hex0[N][65];
