@@ -18,6 +18,7 @@ at the end of the space, 62^9), a window length (2^12..2^19) and a difficulty
 Stops at the first mismatch (no retries) and prints it.  One JSON summary line.
 
     python tests/parity_fuzz.py --cases 300 --seed 7      (test infrastructure: it runs the oracle)
+    POW_LAT_WPS=4 python tests/parity_fuzz.py --test-hooks --cases 2000 --seed 8   (K1' asm variants)
 """
 import argparse
 import hashlib
@@ -128,8 +129,19 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=300)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--test-hooks", action="store_true",
+                    help="run on libpow_gpu_test.so, which reads the test switches (POW_LAT_WPS, POW_FORCE_FULL, "
+                         "POW_LAT_MAX) from the environment")
     args = ap.parse_args()
-    res = run(args.cases, args.seed, progress=lambda s: print(s, flush=True))
+    miner = None
+    if args.test_hooks:
+        from mpi_blockchain_amd.miner import GpuMiner
+
+        miner = GpuMiner(0, test_hooks=True)
+        miner.warmup()
+    res = run(args.cases, args.seed, miner=miner, progress=lambda s: print(s, flush=True))
+    if miner is not None:
+        miner.close()
     print(json.dumps(res), flush=True)
     return 0 if res.get("ok") else 1
 

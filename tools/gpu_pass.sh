@@ -9,6 +9,9 @@
 #   bench            python bench.py (default: N = 1, every block of the JSON line)
 #   profile          tools/profile_round.sh r04 (kernel trace + 4 PMC passes of the bench workload)
 #   fuzz             randomised parity, shipped library: 1,000 cases (tests/parity_fuzz.py)
+#   fuzz_big         10,000 cases, then 2,000 each on the test library: K1' asm variants
+#                    (POW_LAT_WPS=4), + d > 32 variants, and K1 alone (POW_LAT_MAX=0)
+#   soak_mixed       20 mixed networks: 2 reference ranks + 2 pow_node ranks (tools/protocol_soak.py)
 #   ab_k1 L...       K1 sweep A/B over libpow_gpu.so builds (tools/ab_sweep, 9 alternating windows)
 #   ab_k2 L...       pow_hash_block A/B (tools/ab_k2, 5 x 200 calls)
 #   ttb D L...       time-to-block A/B at difficulty D (tools/ab_ttb, 301 templates)
@@ -19,7 +22,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 S="$R/tools/gpu_step.sh"
 L="$R/mpi_blockchain_amd/libpow_gpu.so"
-STEPS=" tests smoke bench profile fuzz ab_k1 ab_k2 ttb k2_trace pmc_onewave "
+STEPS=" tests smoke bench profile fuzz fuzz_big soak_mixed ab_k1 ab_k2 ttb k2_trace pmc_onewave "
 libs() {  # the library arguments of an A/B step
   LIBS=()
   while [ $# -gt 0 ] && [[ "$STEPS" != *" $1 "* ]]; do LIBS+=("$1"); shift; done
@@ -33,6 +36,11 @@ while [ $# -gt 0 ]; do
     bench) $S bench 900 python -u bench.py || exit $? ;;
     profile) bash "$R/tools/profile_round.sh" r04 || exit $? ;;
     fuzz) $S fuzz 900 python -u tests/parity_fuzz.py --cases 1000 --seed 404 || exit $? ;;
+    fuzz_big) $S fuzz_big 900 python -u tests/parity_fuzz.py --cases 10000 --seed 4004 &&
+      POW_LAT_WPS=4 $S fuzz_lat_asm 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4005 &&
+      POW_LAT_WPS=4 POW_FORCE_FULL=1 $S fuzz_lat_asm_full 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4006 &&
+      POW_LAT_MAX=0 $S fuzz_k1only 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4007 || exit $? ;;
+    soak_mixed) $S soak_mixed 900 python -u tools/protocol_soak.py --runs 20 --ranks 2 --ref 2 --difficulty 9 || exit $? ;;
     ab_k1) libs "$@"; shift ${#LIBS[@]}; $S ab_k1 400 tools/ab_sweep 9 "${LIBS[@]}" || exit $? ;;
     ab_k2) libs "$@"; shift ${#LIBS[@]}; $S ab_k2 200 tools/ab_k2 5 "${LIBS[@]}" || exit $? ;;
     ttb) d=$1; shift; libs "$@"; shift ${#LIBS[@]}; $S ttb_d$d 300 tools/ab_ttb "$d" 301 "${LIBS[@]}" || exit $? ;;
