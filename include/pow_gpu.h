@@ -93,6 +93,14 @@ void pow_destroy(pow_ctx* ctx);
 int pow_warmup(pow_ctx* ctx);
 const char* pow_last_error(void);
 int pow_get_stats(const pow_ctx* ctx, pow_stats* out);
+/* How the context launches its latency-bound kernels (the one-block hash of
+ * pow_hash_block and the first sub-round of pow_mine[_any]):
+ * POW_LAUNCH_DIRECT = AQL packets into a queue of its own (no HIP launch call
+ * on the path), POW_LAUNCH_HIP = hipLaunchKernel on the context's stream (the
+ * fallback when the direct queue cannot be set up; same kernels, same
+ * results, ~8 us more per launch).  < 0 = error. */
+enum { POW_LAUNCH_HIP = 0, POW_LAUNCH_DIRECT = 1 };
+int pow_launch_path(const pow_ctx* ctx);
 /* Device properties the roofline uses: CU count and peak engine clock (kHz). */
 int pow_device_info(const pow_ctx* ctx, int* cu_count, int* clock_khz, char* name, size_t name_cap);
 

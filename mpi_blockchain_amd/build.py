@@ -17,8 +17,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libpow_gpu.so")
-SOURCES = ["pow_api.cpp", "pow_board.cpp", "pow_group.cpp", "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip"]
-HEADERS = ["pow_template.h", "sha256_dev.h"]
+SOURCES = ["pow_api.cpp", "pow_aql.cpp", "pow_board.cpp", "pow_group.cpp", "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip"]
+HEADERS = ["pow_template.h", "sha256_dev.h", "pow_aql.h"]
 INCLUDES = [os.path.join(ROOT, "include", h) for h in ("pow_gpu.h", "pow_tools.h")]
 ARCH = "gfx950"
 
@@ -88,7 +88,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
             common.append(os.path.join(OBJ, base + ".o"))
             _compile(s, common[-1], (), verbose)
     for lib, objs in ((LIB, plain), (TEST_LIB, hooked)):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *common, *objs, "-o", lib + ".tmp"]
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *common, *objs, "-o", lib + ".tmp",
+               "-L", "/opt/rocm/lib", "-lhsa-runtime64", "-Wl,-rpath,/opt/rocm/lib"]  # pow_aql.cpp: direct dispatch
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=ROOT)

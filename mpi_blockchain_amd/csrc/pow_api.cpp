@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/pow_gpu.h"
+#include "pow_aql.h"
 #include "pow_template.h"
 
 #ifndef POW_WAIT_POLL_US
@@ -217,6 +218,10 @@ struct pow_ctx {
   uint64_t lat_max = 1ull << 24;  // first-sub-round cap for K1' (0 = K1 only)
   unsigned lat_wps = 0;           // K1' waves per SIMD at every d (0 = the plan)
   bool sentinel_idle = false;     // K1 mine launches: the sentinel wave takes no chunk (POW_LAUNCH_SENTINEL_IDLE)
+  // K1' and K2' launches: packets written into a queue of the context's own
+  // (pow_aql.cpp) instead of hipLaunchKernel; null = the HIP launch path.
+  pow_aql* aql = nullptr;
+  std::string aql_why;            // why aql is null, if it is
   pow_stats stats{};
 };
 
@@ -335,6 +340,75 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   return POW_OK;
 }
 
+// The explicit kernel arguments of a direct dispatch (pow_aql.cpp): the
+// parameters in declaration order, each at its natural alignment.
+struct ArgPack {
+  alignas(8) uint8_t b[2048];
+  uint32_t n = 0;
+  template <class T>
+  void put(const T& v) {
+    n = (n + (uint32_t)alignof(T) - 1) & ~((uint32_t)alignof(T) - 1);
+    memcpy(b + n, &v, sizeof v);
+    n += (uint32_t)sizeof v;
+  }
+};
+
+// Wait for a latency-bound launch to publish `seq` into its done word (mapped
+// host memory): return as soon as it shows, without waiting for the kernel's
+// completion signal (~5 us later; rocprofv3 trace of tools/ttb_c, DESIGN.md
+// §4).  A launch that ends without publishing (a fault, a queue error) is
+// caught by a completion check every 65536 polls (~60 us).
+int wait_published(pow_ctx* ctx, const volatile uint32_t* done, uint32_t seq, const char* what) {
+  for (uint32_t n = 1; __atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE) != seq; ++n) {
+    if ((n & 0xFFFFu) != 0) continue;
+    int st;  // 1 = running, 0 = ended, < 0 = error
+    hipError_t q = hipSuccess;
+    if (ctx->aql) {
+      st = pow_aql_status(ctx->aql);
+    } else {
+      q = hipStreamQuery(ctx->stream);
+      st = q == hipErrorNotReady ? 1 : q == hipSuccess ? 0 : -1;
+    }
+    if (st == 1) continue;
+    if (__atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE) == seq) break;
+    if (st < 0 && ctx->aql) return fail(POW_EHIP, "%s: the dispatch queue reported HSA status 0x%x", what, -st);
+    HIP_OK(q);
+    return fail(POW_EHIP, "%s ended without publishing its result", what);
+  }
+  return POW_OK;
+}
+
+int launch_hash_one(pow_ctx* ctx, const PowMsg& M, uint32_t seq) {
+  if (!ctx->aql) {
+    HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, seq));
+    return POW_OK;
+  }
+  ArgPack a;
+  a.put(M);
+  a.put(ctx->d_one);
+  a.put(seq);
+  if (pow_aql_dispatch(ctx->aql, POW_AQL_HASH_ONE, 1, 64, a.b, a.n))
+    return fail(POW_EHIP, "dispatch of pow_hash_one failed (queue error 0x%x)", -pow_aql_status(ctx->aql));
+  return POW_OK;
+}
+
+int launch_search_lat(pow_ctx* ctx, bool full, bool any, bool asm_groups, unsigned grid, const PowLaunchLat& L) {
+  if (!ctx->aql) {
+    HIP_OK(pow_launch_search_lat(full, any, asm_groups, grid, ctx->stream, ctx->lat_consts, L, ctx->d_lat,
+                                 ctx->d_lat_host));
+    return POW_OK;
+  }
+  ArgPack a;
+  a.put(ctx->lat_consts);
+  a.put(L);
+  a.put(ctx->d_lat);
+  a.put(ctx->d_lat_host);
+  const int k = POW_AQL_LAT0 + (full ? 1 : 0) + (any ? 2 : 0) + (asm_groups ? 4 : 0);
+  if (pow_aql_dispatch(ctx->aql, k, grid, 256, a.b, a.n))
+    return fail(POW_EHIP, "dispatch of pow_search_lat failed (queue error 0x%x)", -pow_aql_status(ctx->aql));
+  return POW_OK;
+}
+
 // One timed launch of the latency kernel K1' over [start, start+count), count <= 2^31.
 int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, bool any,
                    unsigned waves_per_simd) {
@@ -352,6 +426,7 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // A 256-thread workgroup puts one wave on each SIMD of its CU.
   const uint64_t wg_cap = (uint64_t)ctx->cu_count * std::max(1u, std::min(8u, waves_per_simd));
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + 255) / 256, wg_cap));
+  L.nwg = grid;
   if (++ctx->lat_seq == 0) ctx->lat_seq = 1;  // never 0: warm-up launches publish 0
   L.seq = ctx->lat_seq;
   // One dispatch: constants by value (kernarg), result published by the
@@ -361,21 +436,8 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // trials/s, time-to-block 0.2136 -> 0.2125 ms (profiles/r03/ab/ab14_*).  At 1-2 waves per SIMD the kernel is latency-bound and the
   // compiler's interleaving of independent ops serves it better (d = 13:
   // 0.034 -> 0.038 ms with the groups; profiles/r03/ab/ab8_*).
-  HIP_OK(pow_launch_search_lat(diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, ctx->stream,
-                               ctx->lat_consts, L, ctx->d_lat, ctx->d_lat_host));
-  // Return as soon as the result is published: the kernel's completion
-  // signal reaches the host ~5 us after its last wave exits (rocprofv3 trace
-  // of tools/ttb_c).  A launch that ends without publishing
-  // (a fault) is caught by a stream query every 65536 polls.
-  for (uint32_t n = 1; __atomic_load_n(&ctx->h_lat->done, __ATOMIC_ACQUIRE) != L.seq; ++n) {
-    if ((n & 0xFFFFu) == 0) {  // every ~60 us
-      const hipError_t q = hipStreamQuery(ctx->stream);
-      if (q == hipErrorNotReady) continue;
-      if (__atomic_load_n(&ctx->h_lat->done, __ATOMIC_ACQUIRE) == L.seq) break;
-      HIP_OK(q);
-      return fail(POW_EHIP, "latency kernel ended without publishing its result");
-    }
-  }
+  if (int rc = launch_search_lat(ctx, diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, L)) return rc;
+  if (int rc = wait_published(ctx, &ctx->h_lat->done, L.seq, "latency kernel")) return rc;
   memcpy(ctx->h_res, (const void*)ctx->h_lat, sizeof(PowResult));
   const double ms = (double)ctx->h_res->ticks / ctx->realtime_khz;
   ctx->stats.kernel_ms += ms;
@@ -499,6 +561,11 @@ int pow_init(int device, pow_ctx** out) {
     const int per = atoi(g);
     if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
   }
+  const char* no_aql = getenv("POW_NO_AQL");  // K1'/K2' through hipLaunchKernel (A/B, fallback tests)
+  const unsigned aql_flags = getenv("POW_AQL_EXP") ? (unsigned)strtoul(getenv("POW_AQL_EXP"), nullptr, 0) : 0u;
+#else
+  const char* no_aql = nullptr;
+  const unsigned aql_flags = 0;
 #endif
   int rc = POW_OK;
   auto chk = [&](hipError_t e, const char* what) {
@@ -539,6 +606,8 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipHostMalloc(&ctx->h_res, sizeof(PowResult), hipHostMallocDefault), "hipHostMalloc");
   ctx->tail_cap = ctx->grid_full * 4u * 32u;  // < 32 per wave, 4 waves per workgroup
   chk(hipMalloc(&ctx->d_tail, (size_t)ctx->tail_cap * sizeof(uint32_t)), "hipMalloc sweep tail");
+  if (rc == POW_OK && !(no_aql && no_aql[0] == '1') && pow_aql_open(device, aql_flags, &ctx->aql, &ctx->aql_why) != 0)
+    ctx->aql = nullptr;  // the HIP launch path: same kernels, ~8 us more per launch
   if (rc != POW_OK) {
     pow_destroy(ctx);
     return rc;
@@ -551,6 +620,7 @@ void pow_destroy(pow_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  pow_aql_close(ctx->aql);
   (void)hipFree(ctx->d_blob);
   if (ctx->h_blob) (void)hipHostFree(ctx->h_blob);
   (void)hipFree(ctx->d_tail);
@@ -578,6 +648,7 @@ int pow_warmup(pow_ctx* ctx) {
   memset(&L, 0, sizeof L);  // n_prefix = 0: every wave exits at its first dequeue
   PowLaunchLat LL;
   memset(&LL, 0, sizeof LL);  // count = 0
+  LL.nwg = 1;                 // one workgroup: it is the last one out, publishes done = 0 and resets
   for (int mode = 0; mode < 3; ++mode)
     for (int full = 0; full < 2; ++full)
       HIP_OK(pow_launch_search(mode, full != 0, 1, ctx->stream, ctx->d_consts, L, nullptr, ctx->d_res));
@@ -591,9 +662,24 @@ int pow_warmup(pow_ctx* ctx) {
   memset(&M, 0, sizeof M);
   HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, 0));  // publishes done = 0: never a live seq
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (ctx->aql) {  // the same launches once through the direct-dispatch queue (its first packets)
+    for (int k = 0; k < 9; ++k) {
+      if (int rc = k < 8 ? launch_search_lat(ctx, k & 1, k & 2, k & 4, 1, LL) : launch_hash_one(ctx, M, 0)) return rc;
+      for (int st, n = 0; (st = pow_aql_status(ctx->aql)) != 0; ++n) {
+        if (st < 0) return fail(POW_EHIP, "warm-up dispatch: queue error 0x%x", -st);
+        if (n > 20000) break;  // POW_AQL_EXP_NO_SIGNAL (test library): no completion to wait for; ~20 ms
+        std::this_thread::sleep_for(std::chrono::microseconds(1));
+      }
+    }
+  }
   pow_block b;
   memset(&b, 0, sizeof b);
   return pow_hash_blocks(ctx, &b, 1, nullptr, nullptr);
+}
+
+int pow_launch_path(const pow_ctx* ctx) {
+  if (!ctx) return fail(POW_EINVAL, "null");
+  return ctx->aql ? POW_LAUNCH_DIRECT : POW_LAUNCH_HIP;
 }
 
 int pow_get_stats(const pow_ctx* ctx, pow_stats* out) {
@@ -664,18 +750,8 @@ int hash_one(pow_ctx* ctx, const pow_block* b, uint8_t* digest, char* hex) {
   }
   if (++ctx->one_seq == 0) ctx->one_seq = 1;  // never 0: the warm-up launch publishes 0
   const uint32_t seq = ctx->one_seq;
-  HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, seq));
-  // as run_search_lat: return when the result is published; a launch that
-  // ends without publishing (a fault) is caught by a stream query every 65536 polls
-  for (uint32_t n = 1; __atomic_load_n(&ctx->h_one->done, __ATOMIC_ACQUIRE) != seq; ++n) {
-    if ((n & 0xFFFFu) == 0) {
-      const hipError_t q = hipStreamQuery(ctx->stream);
-      if (q == hipErrorNotReady) continue;
-      if (__atomic_load_n(&ctx->h_one->done, __ATOMIC_ACQUIRE) == seq) break;
-      HIP_OK(q);
-      return fail(POW_EHIP, "hash kernel ended without publishing its result");
-    }
-  }
+  if (int rc = launch_hash_one(ctx, M, seq)) return rc;
+  if (int rc = wait_published(ctx, &ctx->h_one->done, seq, "hash kernel")) return rc;
   uint32_t dg[8];
   for (int k = 0; k < 8; ++k) dg[k] = __atomic_load_n(&ctx->h_one->digest[k], __ATOMIC_RELAXED);
   ctx->stats = pow_stats{(double)ctx->h_one->ticks / ctx->realtime_khz, 1u, 1u};

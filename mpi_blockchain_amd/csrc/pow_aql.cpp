@@ -1,0 +1,405 @@
+// Direct AQL dispatch of the one-block and latency kernels (K2' pow_hash_one,
+// K1' pow_search_lat): an HSA queue of the context's own, an AQL kernel-dispatch
+// packet written into it and its doorbell rung, instead of hipLaunchKernel.
+//
+// Why: these launches are latency-bound.  A block validation (pow_hash_block,
+// valid_new_block / validate_block_for_chain, node.cpp:199-253) is ~10 us of
+// kernel on one wave, and the HIP launch path added ~8-13 us around it
+// (hipLaunchKernel alone holds the calling thread ~7 us; DESIGN.md §4 K2').
+// Writing the packet takes well under a microsecond (tools/aql_probe.cpp: the
+// same kernel in the same process, 15.7 us per call against 23.5 us via HIP).
+//
+// What is dispatched is the library's own code: the gfx950 code object is
+// copied out of the offload bundle embedded in this shared library's file (the
+// bundle hipcc linked in, so it cannot be stale), loaded once per device into
+// an HSA executable and looked up by symbol.  Every kernel dispatched here
+// reads only explicit arguments (no hidden ones: K1' takes its workgroup count
+// in PowLaunchLat::nwg), and the loader checks each symbol's kernarg size
+// against the argument structs before anything is dispatched.  Kernel
+// arguments go into a ring of coarse-grained device memory written by the host
+// (then an HDP flush and a read-back, so the packet processor reads them
+// complete).  Every packet has the barrier bit (launches on one queue run in
+// order) and a completion signal (so a launch that ends without publishing its
+// result is still seen).  Any failure to set this up leaves the caller on the
+// HIP launch path (the same kernels).
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pow_aql.h"
+#include "pow_template.h"
+
+namespace {
+
+constexpr uint32_t kQueueSize = 64;    // packets; launches are host-waited, so one is ever in flight
+constexpr uint32_t kSlotBytes = 2048;  // kernel-argument slot (largest: K1', 1,568 B)
+constexpr int kMaxDevices = 64;
+
+const char* kNames[POW_AQL_NKERNELS] = {
+    "_Z12pow_hash_one6PowMsgP10PowHashOutj.kd",
+    "_Z14pow_search_latILb0ELb0ELb0EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb1ELb0ELb0EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb0ELb1ELb0EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb1ELb1ELb0EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb0ELb0ELb1EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb1ELb0ELb1EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb0ELb1ELb1EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+    "_Z14pow_search_latILb1ELb1ELb1EEv12PowConstsLat12PowLaunchLatP9PowResultS3_.kd",
+};
+
+// Explicit argument bytes of each kernel: its parameters in declaration
+// order, each at its natural alignment (the structs are multiples of 8).
+constexpr uint32_t kHashArgs = (uint32_t)(sizeof(PowMsg) + 8 + 4);  // M, hout, seq
+constexpr uint32_t kLatArgs = (uint32_t)(sizeof(PowConstsLat) + sizeof(PowLaunchLat) + 8 + 8);  // C, L, res, hout
+static_assert(sizeof(PowMsg) % 8 == 0 && sizeof(PowConstsLat) % 8 == 0 && sizeof(PowLaunchLat) % 8 == 0,
+              "argument offsets");
+static_assert(kLatArgs <= kSlotBytes && kHashArgs <= kSlotBytes, "slot size");
+
+// The kernels of one device, loaded once per process and kept for its
+// lifetime (an executable torn down beside the HIP runtime's own exit path
+// gains nothing).
+struct DeviceKernels {
+  bool tried = false, ok = false;
+  std::string why;
+  hsa_agent_t agent{};
+  uint32_t* hdp_flush = nullptr;  // HDP_MEM_FLUSH_CNTL: the host's device-memory writes become visible
+  hsa_amd_memory_pool_t coarse{};  // kernel-argument rings
+  bool has_coarse = false;
+  std::vector<hsa_agent_t> cpus;  // given access to the rings
+  struct Kern {
+    uint64_t object = 0;
+    uint32_t kernarg = 0, group = 0, priv = 0;
+  } k[POW_AQL_NKERNELS];
+};
+
+std::mutex g_mu;
+DeviceKernels g_dev[kMaxDevices];
+
+struct AgentSearch {
+  uint32_t bus, dev, domain;
+  hsa_agent_t found{};
+  bool ok = false;
+  std::vector<hsa_agent_t> cpus;
+};
+
+hsa_status_t match_agent(hsa_agent_t a, void* p) {
+  AgentSearch* s = static_cast<AgentSearch*>(p);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_CPU) s->cpus.push_back(a);
+  if (t != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+  hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+  if (!s->ok && ((bdf >> 8) & 0xFF) == s->bus && ((bdf >> 3) & 0x1F) == s->dev && dom == s->domain) {
+    s->found = a;
+    s->ok = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// The device's coarse-grained global pool (where the HIP runtime keeps its own
+// device-side kernel arguments): cached by the kernel's scalar loads, which
+// K1' issues for its 1.4 KB of constants throughout the launch.
+hsa_status_t find_coarse_pool(hsa_amd_memory_pool_t p, void* data) {
+  hsa_amd_segment_t seg;
+  uint32_t flags = 0;
+  bool alloc = false;
+  if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL ||
+      hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS ||
+      !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) ||
+      hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc) != HSA_STATUS_SUCCESS ||
+      !alloc)
+    return HSA_STATUS_SUCCESS;
+  *static_cast<hsa_amd_memory_pool_t*>(data) = p;
+  return HSA_STATUS_INFO_BREAK;
+}
+
+// The gfx950 code object holding the kernels, out of the offload bundles that
+// hipcc embedded in this library's file (one bundle per translation unit with
+// device code; the one naming pow_hash_one is pow_kernels.hip's).
+bool own_code_object(std::vector<char>& out, std::string& why) {
+  Dl_info info;
+  if (!dladdr((const void*)&pow_aql_open, &info) || !info.dli_fname) {
+    why = "dladdr failed";
+    return false;
+  }
+  const int fd = open(info.dli_fname, O_RDONLY);
+  if (fd < 0) {
+    why = std::string("cannot open ") + info.dli_fname;
+    return false;
+  }
+  struct stat st;
+  std::vector<char> file;
+  if (fstat(fd, &st) == 0 && st.st_size > 0) {
+    file.resize((size_t)st.st_size);
+    size_t got = 0;
+    while (got < file.size()) {
+      const ssize_t n = read(fd, file.data() + got, file.size() - got);
+      if (n <= 0) break;
+      got += (size_t)n;
+    }
+    file.resize(got);
+  }
+  close(fd);
+  static const char kMagic[] = "__CLANG_OFFLOAD_BUNDLE__";
+  static const char kTriple[] = "hipv4-amdgcn-amd-amdhsa--gfx950";
+  static const char kNeedle[] = "_Z12pow_hash_one";
+  const char* base = file.data();
+  const size_t n = file.size();
+  for (size_t i = 0; i + 32 <= n; ++i) {
+    if (memcmp(base + i, kMagic, 24) != 0) continue;
+    uint64_t entries = 0;
+    memcpy(&entries, base + i + 24, 8);
+    size_t off = i + 32;
+    for (uint64_t e = 0; e < entries && e < 16 && off + 24 <= n; ++e) {
+      uint64_t o = 0, sz = 0, tl = 0;
+      memcpy(&o, base + off, 8);
+      memcpy(&sz, base + off + 8, 8);
+      memcpy(&tl, base + off + 16, 8);
+      off += 24;
+      if (tl > 256 || off + tl > n) break;
+      const std::string triple(base + off, (size_t)tl);
+      off += tl;
+      if (triple != kTriple || sz == 0 || o > n - i || sz > n - i - o) continue;
+      const char* co = base + i + o;
+      if (std::search(co, co + sz, kNeedle, kNeedle + sizeof kNeedle - 1) == co + sz) continue;
+      out.assign(co, co + sz);
+      return true;
+    }
+  }
+  why = "no gfx950 code object with the kernels in the library's offload bundles";
+  return false;
+}
+
+// Load (once) the kernels for `device`; the caller holds g_mu.
+const DeviceKernels* device_kernels(int device) {
+  DeviceKernels& D = g_dev[device];
+  if (D.tried) return &D;
+  D.tried = true;
+  auto bail = [&](const std::string& why) {
+    D.why = why;
+    return &D;
+  };
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail("hipGetDeviceProperties");
+  if (hsa_init() != HSA_STATUS_SUCCESS) return bail("hsa_init");  // reference-counted; the HIP runtime holds one
+  AgentSearch s{(uint32_t)prop.pciBusID, (uint32_t)prop.pciDeviceID, (uint32_t)prop.pciDomainID};
+  if (hsa_iterate_agents(match_agent, &s) != HSA_STATUS_SUCCESS || !s.ok) return bail("no HSA agent for the device");
+  D.agent = s.found;
+  D.cpus = s.cpus;
+  D.has_coarse = !D.cpus.empty() &&
+                 hsa_amd_agent_iterate_memory_pools(D.agent, find_coarse_pool, &D.coarse) == HSA_STATUS_INFO_BREAK;
+  std::vector<char>* code = new std::vector<char>;  // kept: the reader may refer to it
+  if (!own_code_object(*code, D.why)) return bail(D.why);
+  hsa_code_object_reader_t reader;
+  hsa_executable_t exe;
+  if (hsa_code_object_reader_create_from_memory(code->data(), code->size(), &reader) != HSA_STATUS_SUCCESS)
+    return bail("hsa_code_object_reader_create_from_memory");
+  if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe) !=
+      HSA_STATUS_SUCCESS)
+    return bail("hsa_executable_create_alt");
+  if (hsa_executable_load_agent_code_object(exe, D.agent, reader, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+      hsa_executable_freeze(exe, nullptr) != HSA_STATUS_SUCCESS)
+    return bail("loading the code object");
+  for (int i = 0; i < POW_AQL_NKERNELS; ++i) {
+    hsa_executable_symbol_t sym;
+    DeviceKernels::Kern& K = D.k[i];
+    if (hsa_executable_get_symbol_by_name(exe, kNames[i], &D.agent, &sym) != HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &K.object) !=
+            HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &K.kernarg) !=
+            HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &K.group) !=
+            HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &K.priv) !=
+            HSA_STATUS_SUCCESS)
+      return bail(std::string("symbol ") + kNames[i]);
+    // The bytes the host writes must be exactly what the kernel reads: explicit
+    // arguments only (a kernel with hidden arguments has a larger segment).
+    if (K.kernarg != (i == POW_AQL_HASH_ONE ? kHashArgs : kLatArgs))
+      return bail(std::string("kernarg size of ") + kNames[i] + " is " + std::to_string(K.kernarg));
+  }
+  hsa_amd_hdp_flush_t hdp{};
+  if (hsa_agent_get_info(D.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) != HSA_STATUS_SUCCESS ||
+      !hdp.HDP_MEM_FLUSH_CNTL)
+    return bail("no HDP flush register");
+  D.hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
+  D.ok = true;
+  return &D;
+}
+
+}  // namespace
+
+struct pow_aql {
+  const DeviceKernels* dk = nullptr;
+  unsigned flags = 0;        // POW_AQL_EXP_* (test library experiments)
+  hsa_queue_t* q = nullptr;
+  hsa_signal_t done{};       // completion signal: the number of launches in flight
+  bool signal_up = false;
+  uint8_t* ring = nullptr;   // kernel-argument slots: device memory the host writes
+  int ring_kind = 0;         // 1 host, 2 fine-grained device, 3 coarse-grained device (the default)
+  std::atomic<int> queue_error{0};
+};
+
+namespace {
+void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
+  static_cast<pow_aql*>(data)->queue_error.store((int)st, std::memory_order_release);
+}
+}  // namespace
+
+int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
+  *out = nullptr;
+  if (device < 0 || device >= kMaxDevices) {
+    if (why) *why = "device index";
+    return -1;
+  }
+  const DeviceKernels* dk;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    dk = device_kernels(device);
+  }
+  if (!dk->ok) {
+    if (why) *why = dk->why;
+    return -1;
+  }
+  pow_aql* a = new pow_aql;
+  a->dk = dk;
+  a->flags = flags;
+  auto bail = [&](const char* w) {
+    if (why) *why = w;
+    pow_aql_close(a);
+    return -1;
+  };
+  const size_t ring_bytes = (size_t)kQueueSize * kSlotBytes;
+  if (flags & POW_AQL_EXP_HOST_ARGS) {
+    a->ring_kind = 1;
+    if (hipHostMalloc((void**)&a->ring, ring_bytes, hipHostMallocCoherent) != hipSuccess)
+      return bail("kernel-argument ring");
+  } else if (flags & (POW_AQL_EXP_FINE_ARGS | POW_AQL_EXP_UNCACHED_ARGS)) {
+    a->ring_kind = 2;
+    if (hipExtMallocWithFlags((void**)&a->ring, ring_bytes,
+                              (flags & POW_AQL_EXP_UNCACHED_ARGS) ? hipDeviceMallocUncached
+                                                                  : hipDeviceMallocFinegrained) != hipSuccess)
+      return bail("kernel-argument ring");
+  } else {
+    // coarse-grained device memory the host writes through the BAR
+    a->ring_kind = 3;
+    if (!dk->has_coarse) return bail("no coarse-grained device pool");
+    if (hsa_amd_memory_pool_allocate(dk->coarse, ring_bytes, 0, (void**)&a->ring) != HSA_STATUS_SUCCESS) {
+      a->ring = nullptr;
+      return bail("kernel-argument ring");
+    }
+    if (hsa_amd_agents_allow_access((uint32_t)dk->cpus.size(), dk->cpus.data(), nullptr, a->ring) !=
+        HSA_STATUS_SUCCESS)
+      return bail("host access to the kernel-argument ring");
+  }
+  // A signal only the GPU's packet processor writes and the host reads: no
+  // interrupt event behind it (the host never sleeps on it).
+  if (hsa_amd_signal_create(0, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &a->done) != HSA_STATUS_SUCCESS &&
+      hsa_signal_create(0, 0, nullptr, &a->done) != HSA_STATUS_SUCCESS)
+    return bail("completion signal");
+  a->signal_up = true;
+  if (hsa_queue_create(dk->agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a, UINT32_MAX, UINT32_MAX,
+                       &a->q) != HSA_STATUS_SUCCESS)
+    return bail("hsa_queue_create");
+  *out = a;
+  return 0;
+}
+
+void pow_aql_close(pow_aql* a) {
+  if (!a) return;
+  if (a->q) {
+    // Launches are host-waited, so the queue is idle here unless one failed
+    // mid-flight: wait (bounded) for the last one to complete.
+    for (int n = 0; n < 1000000 && a->signal_up && hsa_signal_load_scacquire(a->done) != 0 &&
+                    !a->queue_error.load(std::memory_order_acquire);
+         ++n)
+      usleep(1);
+    hsa_queue_destroy(a->q);
+  }
+  if (a->signal_up) hsa_signal_destroy(a->done);
+  if (a->ring) {
+    if (a->ring_kind == 1) (void)hipHostFree(a->ring);
+    else if (a->ring_kind == 2) (void)hipFree(a->ring);
+    else hsa_amd_memory_pool_free(a->ring);
+  }
+  delete a;
+}
+
+int pow_aql_status(const pow_aql* a) {
+  const int e = a->queue_error.load(std::memory_order_acquire);
+  if (e) return -e;
+  if (a->flags & POW_AQL_EXP_NO_SIGNAL) return 1;
+  return hsa_signal_load_scacquire(a->done) == 0 ? 0 : 1;
+}
+
+int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_size, const void* args,
+                     uint32_t nbytes) {
+  if (kernel < 0 || kernel >= POW_AQL_NKERNELS || !args || workgroups == 0 || wg_size == 0 || wg_size > 1024 ||
+      (uint64_t)workgroups * wg_size > 0xFFFFFFFFull)
+    return -1;
+  const DeviceKernels::Kern& K = a->dk->k[kernel];
+  if (nbytes != K.kernarg || a->queue_error.load(std::memory_order_acquire)) return -1;
+  hsa_queue_t* q = a->q;
+  const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
+  // The slot is free once the packet processor has read past idx - size
+  // (launches are host-waited, so this never waits in practice).
+  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size)
+    if (a->queue_error.load(std::memory_order_acquire)) return -1;
+  uint8_t* arg = a->ring + (size_t)kSlotBytes * (idx % q->size);
+  memcpy(arg, args, nbytes);
+  // Device memory written over PCIe: drain the write-combining buffers, flush
+  // the HDP, and read a word back, so the kernel reads the new arguments.
+  __builtin_ia32_sfence();
+  if (a->flags & POW_AQL_EXP_READBACK_ONLY) {
+    // no HDP flush: store the last word again, full fence, read it back
+    memcpy(arg + nbytes - 4, (const uint8_t*)args + nbytes - 4, 4);
+    __builtin_ia32_mfence();
+    (void)*(volatile uint32_t*)(arg + nbytes - 4);
+    __builtin_ia32_lfence();
+  } else if (!(a->flags & (POW_AQL_EXP_NO_FLUSH | POW_AQL_EXP_HOST_ARGS))) {
+    *(volatile uint32_t*)a->dk->hdp_flush = 1u;
+    if (!(a->flags & POW_AQL_EXP_NO_READBACK)) (void)*(volatile uint32_t*)(arg + nbytes - 4);
+  }
+  // in flight += 1; the packet processor subtracts 1 when the launch
+  // completes (which may be after the caller has seen the kernel's done word
+  // and started the next launch: a count, not a flag)
+  const bool sig = !(a->flags & POW_AQL_EXP_NO_SIGNAL);
+  if (sig) hsa_signal_add_scacq_screl(a->done, 1);
+  hsa_kernel_dispatch_packet_t* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx % q->size);
+  memset((uint8_t*)pk + 4, 0, sizeof *pk - 4);  // everything but header + setup, which go last
+  pk->workgroup_size_x = (uint16_t)wg_size;
+  pk->workgroup_size_y = 1;
+  pk->workgroup_size_z = 1;
+  pk->grid_size_x = workgroups * wg_size;
+  pk->grid_size_y = 1;
+  pk->grid_size_z = 1;
+  pk->private_segment_size = K.priv;
+  pk->group_segment_size = K.group;
+  pk->kernel_object = K.object;
+  pk->kernarg_address = arg;
+  if (sig) pk->completion_signal = a->done;
+  const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                     ((a->flags & POW_AQL_EXP_NO_BARRIER) ? 0 : (1 << HSA_PACKET_HEADER_BARRIER)) |
+                                     (((a->flags & POW_AQL_EXP_ACQUIRE_AGENT) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM)
+                                      << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                     (((a->flags & POW_AQL_EXP_RELEASE_AGENT) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM)
+                                      << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  __atomic_store_n((uint32_t*)pk, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
+  return 0;
+}

@@ -1,0 +1,41 @@
+// Direct AQL dispatch of the latency-bound kernels (pow_aql.cpp).  Internal to
+// libpow_gpu.so: not part of the C ABI.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+
+struct pow_aql;
+
+enum {
+  POW_AQL_HASH_ONE = 0,  // K2' pow_hash_one(PowMsg, PowHashOut*, uint32_t)
+  POW_AQL_LAT0 = 1,      // K1' pow_search_lat<FULL, ANY, ASM>: POW_AQL_LAT0 + (FULL | ANY << 1 | ASM << 2)
+  POW_AQL_NKERNELS = 9
+};
+
+// A queue of its own on `device` (the kernels are loaded once per device per
+// process).  0 = ready; -1 = not available here (*why says why; the caller
+// keeps the HIP launch path).
+int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why);
+// Dispatch experiments (flags of pow_aql_open; the shipped library passes 0,
+// the test library POW_AQL_EXP from the environment).
+enum {
+  POW_AQL_EXP_NO_SIGNAL = 1,    // no completion signal (a launch that ends unpublished then hangs the wait)
+  POW_AQL_EXP_NO_FLUSH = 2,     // no HDP flush / read-back after writing the arguments
+  POW_AQL_EXP_NO_READBACK = 4,  // HDP flush, no read-back
+  POW_AQL_EXP_HOST_ARGS = 8,    // arguments in coherent host memory instead of device memory
+  POW_AQL_EXP_NO_BARRIER = 16,  // packets without the barrier bit
+  POW_AQL_EXP_READBACK_ONLY = 32,  // no HDP flush: re-store the last word, mfence, read it back
+  POW_AQL_EXP_FINE_ARGS = 64,   // arguments in fine-grained device memory
+  POW_AQL_EXP_ACQUIRE_AGENT = 128,  // packet acquire fence at agent scope (no L2 invalidate)
+  POW_AQL_EXP_RELEASE_AGENT = 256,  // packet release fence at agent scope (no L2 write-back)
+  POW_AQL_EXP_UNCACHED_ARGS = 512,  // arguments in uncached device memory
+};
+void pow_aql_close(pow_aql* a);
+// 0 = the last launch completed, 1 = still running, < 0 = the queue reported
+// an error (minus the HSA status).
+int pow_aql_status(const pow_aql* a);
+// One packet: `workgroups` x `wg_size` work-items of `kernel`, its explicit
+// arguments `args` (exactly the kernel's kernarg size).  0 = dispatched.
+int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_size, const void* args,
+                     uint32_t nbytes);

@@ -647,7 +647,7 @@ __global__ __launch_bounds__(256) void pow_search_lat(
   const cptr Cb = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-  const uint32_t nwaves = gridDim.x * 4u;
+  const uint32_t nwaves = L.nwg * 4u;  // L.nwg == gridDim.x (no implicit kernel argument needed)
   uint32_t iters = 0;
   bool wrote_hit = false;  // this wave wrote a hit record (wave-uniform after each step)
   __shared__ uint32_t wg_iters;  // wave-iterations of this workgroup
@@ -767,7 +767,7 @@ __global__ __launch_bounds__(256) void pow_search_lat(
       old = __hip_atomic_fetch_add(&res->hashes, ((unsigned long long)wg_iters << 32) | 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
     old = uniform64(old);
-    if ((uint32_t)old == gridDim.x - 1u) {
+    if ((uint32_t)old == L.nwg - 1u) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const uint32_t nh = res->nhit < POW_HITS ? res->nhit : POW_HITS;
       if (lane < nh) {  // one lane per recorded hit

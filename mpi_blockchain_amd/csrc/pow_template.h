@@ -102,6 +102,8 @@ struct PowLaunchLat {
   uint32_t seq;            // launch sequence number, published last (PowResult::done)
   uint64_t count;          // counters [ctr_start, ctr_start + count), count <= 2^31
   PowWatch watch;
+  uint32_t nwg;            // workgroups of the launch (= gridDim.x): passed explicitly so the
+  uint32_t pad;            // kernel reads no implicit argument (direct AQL dispatch, pow_aql.cpp)
 };
 
 struct PowLaunch {

@@ -80,6 +80,11 @@ class GpuMiner:
         check(self.L.pow_device_info(self.ctx, ctypes.byref(cu), ctypes.byref(clk), name, 256), self.L)
         return {"cu_count": cu.value, "clock_khz": clk.value, "name": name.value.decode()}
 
+    def launch_path(self) -> str:
+        """"direct" (AQL packets into the context's own queue) or "hip"
+        (hipLaunchKernel) for the latency-bound launches (pow_launch_path)."""
+        return "direct" if check(self.L.pow_launch_path(self.ctx), self.L) == 1 else "hip"
+
     def stats(self) -> dict:
         s = PowStats()
         check(self.L.pow_get_stats(self.ctx, ctypes.byref(s)), self.L)

@@ -39,7 +39,7 @@ def test_library_exports_all_symbols():
 
 
 HOOKS = (b"POW_FAULT_INJECT", b"POW_FORCE_FULL", b"POW_LAT_MAX", b"POW_LAT_WPS", b"POW_GRID_PER_CU", b"POW_TEST_SENTINEL_IDLE",
-         b"POW_TEST_RCCL_LIB")
+         b"POW_TEST_RCCL_LIB", b"POW_NO_AQL", b"POW_AQL_EXP")
 
 
 def test_shipped_library_has_no_test_hooks():

@@ -116,6 +116,30 @@ def test_single_block_path(miner, golden, templates):
     assert statistics.median(lat) < 0.001, lat
 
 
+def test_launch_paths(miner, golden, templates):
+    """The latency-bound launches (K2' here, K1' in pow_mine's first sub-round)
+    go out as AQL packets on the context's own queue (pow_aql.cpp) in the
+    shipped library; the test library's POW_NO_AQL=1 keeps them on
+    hipLaunchKernel, the fallback.  Both give the reference's digests and the
+    same lowest solution."""
+    assert miner.launch_path() == "direct"
+    hip = hooked_miner(POW_NO_AQL=1)
+    try:
+        assert hip.launch_path() == "hip"
+        for e in golden["random_blocks"]:
+            b = block_from_random(e)
+            assert hip.block_to_hash(b) == miner.block_to_hash(b) == e["hex"]
+        w = golden["windows"][0]
+        b = block_from_template(templates[w["template"]])
+        for d, st in w["sets"].items():
+            if st["count"]:
+                want = w["start"] + st["counters"][0]
+                assert miner.mine(b, w["start"], w["count"], int(d)).counter == want
+                assert hip.mine(b, w["start"], w["count"], int(d)).counter == want
+    finally:
+        hip.close()
+
+
 def test_messages(golden, templates):
     for name, hx in golden["messages"].items():
         b = with_nonce(block_from_template(templates[name]), nonce_from_counter(0))
@@ -481,13 +505,15 @@ def test_parity_fuzz():
     assert res["cases"] == 120 and res["solutions"] > 0
 
 
-@pytest.mark.parametrize("env", [{"POW_LAT_WPS": 4}, {"POW_LAT_WPS": 4, "POW_FORCE_FULL": 1}],
-                         ids=["lat_asm", "lat_asm_full"])
+@pytest.mark.parametrize("env", [{"POW_LAT_WPS": 4}, {"POW_LAT_WPS": 4, "POW_FORCE_FULL": 1}, {"POW_NO_AQL": 1}],
+                         ids=["lat_asm", "lat_asm_full", "hip_launch"])
 def test_parity_fuzz_latency_asm_variants(env):
     """The latency kernel's asm-group variants (pow_search_lat<*, *, true>, run
     by the plan only at d = 20-21, 4 waves per SIMD) under the same exact
     oracle comparison: the test library forces 4 waves per SIMD at every d,
-    and with POW_FORCE_FULL the d > 32 variants <true, *, true> as well."""
+    and with POW_FORCE_FULL the d > 32 variants <true, *, true> as well.
+    hip_launch: the plan's kernels launched through hipLaunchKernel (the
+    fallback when the direct dispatch queue cannot be set up)."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import parity_fuzz
 

@@ -22,6 +22,30 @@ typedef int (*stats_fn)(const pow_ctx*, pow_stats*);
 #define N 200
 #define MAXL 8
 
+/* A library argument may carry environment settings for its pow_init:
+ * "path@VAR=VAL,VAR=VAL" (the test library's switches).  Sets them;
+ * env_clear() unsets them after the context exists. */
+static char env_names[8][64];
+static int env_n = 0;
+static void env_apply(const char* spec) {
+  static char buf[512];
+  snprintf(buf, sizeof buf, "%s", spec);
+  char* at = strchr(buf, '@');
+  env_n = 0;
+  if (!at) return;
+  for (char* kv = strtok(at + 1, ","); kv && env_n < 8; kv = strtok(NULL, ",")) {
+    char* eq = strchr(kv, '=');
+    if (!eq) continue;
+    *eq = 0;
+    snprintf(env_names[env_n++], 64, "%s", kv);
+    setenv(kv, eq + 1, 1);
+  }
+}
+static void env_clear(void) {
+  for (int i = 0; i < env_n; ++i) unsetenv(env_names[i]);
+  env_n = 0;
+}
+
 static int cmp(const void* a, const void* b) {
   double x = *(const double*)a, y = *(const double*)b;
   return x < y ? -1 : x > y;
@@ -48,7 +72,12 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 64; ++k) blk[i].previous_block_hash[k] = "0123456789abcdef"[(i + k * 5) % 16];
   }
   for (int l = 0; l < nl; ++l) {
-    void* h = dlopen(argv[2 + l], RTLD_NOW | RTLD_LOCAL);
+    char path[512];
+    snprintf(path, sizeof path, "%s", argv[2 + l]);
+    char* at = strchr(path, '@');
+    env_apply(argv[2 + l]);
+    if (at) *at = 0;
+    void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     if (!h) {
       fprintf(stderr, "%s\n", dlerror());
       return 1;
@@ -58,6 +87,7 @@ int main(int argc, char** argv) {
     hash[l] = (hash_fn)dlsym(h, "pow_hash_block");
     stats[l] = (stats_fn)dlsym(h, "pow_get_stats");
     if (init(0, &ctx[l]) || warm(ctx[l])) return 1;
+    env_clear();
     /* AB_K2_IDLE_CTX=n: n more contexts of this library that never hash (their streams exist) */
     const char* e = getenv("AB_K2_IDLE_CTX");
     for (int k = 0; e && k < atoi(e); ++k) {

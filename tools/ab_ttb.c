@@ -21,6 +21,30 @@ typedef int (*any_fn)(pow_ctx*, const pow_block*, uint64_t, uint64_t, unsigned, 
                       pow_block*, uint64_t*, uint64_t*);
 typedef int (*stats_fn)(const pow_ctx*, pow_stats*);
 
+/* A library argument may carry environment settings for its pow_init:
+ * "path@VAR=VAL,VAR=VAL" (the test library's switches).  Sets them;
+ * env_clear() unsets them after the context exists. */
+static char env_names[8][64];
+static int env_n = 0;
+static void env_apply(const char* spec) {
+  static char buf[512];
+  snprintf(buf, sizeof buf, "%s", spec);
+  char* at = strchr(buf, '@');
+  env_n = 0;
+  if (!at) return;
+  for (char* kv = strtok(at + 1, ","); kv && env_n < 8; kv = strtok(NULL, ",")) {
+    char* eq = strchr(kv, '=');
+    if (!eq) continue;
+    *eq = 0;
+    snprintf(env_names[env_n++], 64, "%s", kv);
+    setenv(kv, eq + 1, 1);
+  }
+}
+static void env_clear(void) {
+  for (int i = 0; i < env_n; ++i) unsetenv(env_names[i]);
+  env_n = 0;
+}
+
 static double now(void) {
   struct timespec t;
   clock_gettime(CLOCK_MONOTONIC, &t);
@@ -45,7 +69,12 @@ int main(int argc, char** argv) {
   static double wall[8][1001];
   double kms[8] = {0}, hashes[8] = {0};
   for (int v = 0; v < nv; ++v) {
-    void* h = dlopen(argv[3 + v], RTLD_NOW | RTLD_LOCAL);
+    char path[512];
+    snprintf(path, sizeof path, "%s", argv[3 + v]);
+    char* at = strchr(path, '@');
+    env_apply(argv[3 + v]);
+    if (at) *at = 0;
+    void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     if (!h) {
       fprintf(stderr, "%s\n", dlerror());
       return 1;
@@ -61,6 +90,7 @@ int main(int argc, char** argv) {
       fprintf(stderr, "init failed for %s\n", argv[3 + v]);
       return 1;
     }
+    env_clear();
   }
   srand(1);
   for (int k = -5; k < nt; ++k) { /* k < 0: untimed warm-up templates */
