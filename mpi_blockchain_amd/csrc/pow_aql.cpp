@@ -4,10 +4,9 @@
 //
 // Why: these launches are latency-bound.  A block validation (pow_hash_block,
 // valid_new_block / validate_block_for_chain, node.cpp:199-253) is ~10 us of
-// kernel on one wave, and the HIP launch path added ~8-13 us around it
-// (hipLaunchKernel alone holds the calling thread ~7 us; DESIGN.md §4 K2').
-// Writing the packet takes well under a microsecond (tools/aql_probe.cpp: the
-// same kernel in the same process, 15.7 us per call against 23.5 us via HIP).
+// kernel on one wave, and the HIP launch path adds ~8-10 us around it, with a
+// wide spread from process to process (DESIGN.md §4 K2').  Writing the packet
+// takes ~2 us, most of it the PCIe read-back below.
 //
 // What is dispatched is the library's own code: the gfx950 code object is
 // copied out of the offload bundle embedded in this shared library's file (the
@@ -15,13 +14,23 @@
 // an HSA executable and looked up by symbol.  Every kernel dispatched here
 // reads only explicit arguments (no hidden ones: K1' takes its workgroup count
 // in PowLaunchLat::nwg), and the loader checks each symbol's kernarg size
-// against the argument structs before anything is dispatched.  Kernel
-// arguments go into a ring of coarse-grained device memory written by the host
-// (then an HDP flush and a read-back, so the packet processor reads them
-// complete).  Every packet has the barrier bit (launches on one queue run in
-// order) and a completion signal (so a launch that ends without publishing its
-// result is still seen).  Any failure to set this up leaves the caller on the
-// HIP launch path (the same kernels).
+// against the argument structs before anything is dispatched.
+//
+// Memory protocol of a dispatch:
+//  * arguments: a ring of device memory, uncached on the GPU side, written by
+//    the host through the BAR; then an HDP flush and a read-back of the last
+//    word, so they are in HBM before the doorbell;
+//  * acquire fence at AGENT scope: no L2 invalidate at the start of every
+//    launch (at system scope K1' at d = 9 ran 17 us instead of 15: its code
+//    and tables came from HBM again).  Nothing the kernels read needs it: the
+//    arguments are uncached, the result words (PowResult) are written by the
+//    previous launch on this device, and host-memory words (cancel epoch, stop
+//    board) are read with system-scope atomics in the kernels;
+//  * release fence at system scope, barrier bit (launches on one queue run in
+//    order), and a completion signal counting launches in flight, so a launch
+//    that ends without publishing its result is still seen.
+// Any failure to set this up leaves the caller on the HIP launch path (the
+// same kernels).
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -74,9 +83,6 @@ struct DeviceKernels {
   std::string why;
   hsa_agent_t agent{};
   uint32_t* hdp_flush = nullptr;  // HDP_MEM_FLUSH_CNTL: the host's device-memory writes become visible
-  hsa_amd_memory_pool_t coarse{};  // kernel-argument rings
-  bool has_coarse = false;
-  std::vector<hsa_agent_t> cpus;  // given access to the rings
   struct Kern {
     uint64_t object = 0;
     uint32_t kernarg = 0, group = 0, priv = 0;
@@ -90,15 +96,13 @@ struct AgentSearch {
   uint32_t bus, dev, domain;
   hsa_agent_t found{};
   bool ok = false;
-  std::vector<hsa_agent_t> cpus;
 };
 
 hsa_status_t match_agent(hsa_agent_t a, void* p) {
   AgentSearch* s = static_cast<AgentSearch*>(p);
   hsa_device_type_t t;
-  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
-  if (t == HSA_DEVICE_TYPE_CPU) s->cpus.push_back(a);
-  if (t != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
   uint32_t bdf = 0, dom = 0;
   hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
   hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
@@ -107,24 +111,6 @@ hsa_status_t match_agent(hsa_agent_t a, void* p) {
     s->ok = true;
   }
   return HSA_STATUS_SUCCESS;
-}
-
-// The device's coarse-grained global pool (where the HIP runtime keeps its own
-// device-side kernel arguments): cached by the kernel's scalar loads, which
-// K1' issues for its 1.4 KB of constants throughout the launch.
-hsa_status_t find_coarse_pool(hsa_amd_memory_pool_t p, void* data) {
-  hsa_amd_segment_t seg;
-  uint32_t flags = 0;
-  bool alloc = false;
-  if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
-      seg != HSA_AMD_SEGMENT_GLOBAL ||
-      hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS ||
-      !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) ||
-      hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc) != HSA_STATUS_SUCCESS ||
-      !alloc)
-    return HSA_STATUS_SUCCESS;
-  *static_cast<hsa_amd_memory_pool_t*>(data) = p;
-  return HSA_STATUS_INFO_BREAK;
 }
 
 // The gfx950 code object holding the kernels, out of the offload bundles that
@@ -199,9 +185,6 @@ const DeviceKernels* device_kernels(int device) {
   AgentSearch s{(uint32_t)prop.pciBusID, (uint32_t)prop.pciDeviceID, (uint32_t)prop.pciDomainID};
   if (hsa_iterate_agents(match_agent, &s) != HSA_STATUS_SUCCESS || !s.ok) return bail("no HSA agent for the device");
   D.agent = s.found;
-  D.cpus = s.cpus;
-  D.has_coarse = !D.cpus.empty() &&
-                 hsa_amd_agent_iterate_memory_pools(D.agent, find_coarse_pool, &D.coarse) == HSA_STATUS_INFO_BREAK;
   std::vector<char>* code = new std::vector<char>;  // kept: the reader may refer to it
   if (!own_code_object(*code, D.why)) return bail(D.why);
   hsa_code_object_reader_t reader;
@@ -250,7 +233,7 @@ struct pow_aql {
   hsa_signal_t done{};       // completion signal: the number of launches in flight
   bool signal_up = false;
   uint8_t* ring = nullptr;   // kernel-argument slots: device memory the host writes
-  int ring_kind = 0;         // 1 host, 2 fine-grained device, 3 coarse-grained device (the default)
+  int ring_kind = 0;         // 1 host memory, 2 device memory
   std::atomic<int> queue_error{0};
 };
 
@@ -288,23 +271,15 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
     a->ring_kind = 1;
     if (hipHostMalloc((void**)&a->ring, ring_bytes, hipHostMallocCoherent) != hipSuccess)
       return bail("kernel-argument ring");
-  } else if (flags & (POW_AQL_EXP_FINE_ARGS | POW_AQL_EXP_UNCACHED_ARGS)) {
+  } else {
+    // Device memory the host writes through the BAR, uncached on the GPU
+    // side: no L2 line can hold a slot's previous arguments, so the packets
+    // need no L2 invalidate (agent-scope acquire; see pow_aql_dispatch).
     a->ring_kind = 2;
     if (hipExtMallocWithFlags((void**)&a->ring, ring_bytes,
-                              (flags & POW_AQL_EXP_UNCACHED_ARGS) ? hipDeviceMallocUncached
-                                                                  : hipDeviceMallocFinegrained) != hipSuccess)
+                              (flags & POW_AQL_EXP_FINE_ARGS) ? hipDeviceMallocFinegrained
+                                                              : hipDeviceMallocUncached) != hipSuccess)
       return bail("kernel-argument ring");
-  } else {
-    // coarse-grained device memory the host writes through the BAR
-    a->ring_kind = 3;
-    if (!dk->has_coarse) return bail("no coarse-grained device pool");
-    if (hsa_amd_memory_pool_allocate(dk->coarse, ring_bytes, 0, (void**)&a->ring) != HSA_STATUS_SUCCESS) {
-      a->ring = nullptr;
-      return bail("kernel-argument ring");
-    }
-    if (hsa_amd_agents_allow_access((uint32_t)dk->cpus.size(), dk->cpus.data(), nullptr, a->ring) !=
-        HSA_STATUS_SUCCESS)
-      return bail("host access to the kernel-argument ring");
   }
   // A signal only the GPU's packet processor writes and the host reads: no
   // interrupt event behind it (the host never sleeps on it).
@@ -331,11 +306,7 @@ void pow_aql_close(pow_aql* a) {
     hsa_queue_destroy(a->q);
   }
   if (a->signal_up) hsa_signal_destroy(a->done);
-  if (a->ring) {
-    if (a->ring_kind == 1) (void)hipHostFree(a->ring);
-    else if (a->ring_kind == 2) (void)hipFree(a->ring);
-    else hsa_amd_memory_pool_free(a->ring);
-  }
+  if (a->ring) (void)(a->ring_kind == 1 ? hipHostFree(a->ring) : hipFree(a->ring));
   delete a;
 }
 
@@ -394,7 +365,7 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
   if (sig) pk->completion_signal = a->done;
   const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                      ((a->flags & POW_AQL_EXP_NO_BARRIER) ? 0 : (1 << HSA_PACKET_HEADER_BARRIER)) |
-                                     (((a->flags & POW_AQL_EXP_ACQUIRE_AGENT) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM)
+                                     (((a->flags & POW_AQL_EXP_ACQUIRE_SYSTEM) ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT)
                                       << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                      (((a->flags & POW_AQL_EXP_RELEASE_AGENT) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM)
                                       << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));

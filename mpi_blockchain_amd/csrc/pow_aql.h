@@ -26,10 +26,9 @@ enum {
   POW_AQL_EXP_HOST_ARGS = 8,    // arguments in coherent host memory instead of device memory
   POW_AQL_EXP_NO_BARRIER = 16,  // packets without the barrier bit
   POW_AQL_EXP_READBACK_ONLY = 32,  // no HDP flush: re-store the last word, mfence, read it back
-  POW_AQL_EXP_FINE_ARGS = 64,   // arguments in fine-grained device memory
-  POW_AQL_EXP_ACQUIRE_AGENT = 128,  // packet acquire fence at agent scope (no L2 invalidate)
-  POW_AQL_EXP_RELEASE_AGENT = 256,  // packet release fence at agent scope (no L2 write-back)
-  POW_AQL_EXP_UNCACHED_ARGS = 512,  // arguments in uncached device memory
+  POW_AQL_EXP_FINE_ARGS = 64,   // arguments in fine-grained device memory (cached in L2)
+  POW_AQL_EXP_ACQUIRE_SYSTEM = 128,  // packet acquire fence at system scope (L2 invalidate)
+  POW_AQL_EXP_RELEASE_AGENT = 256,   // packet release fence at agent scope (no L2 write-back)
 };
 void pow_aql_close(pow_aql* a);
 // 0 = the last launch completed, 1 = still running, < 0 = the queue reported
