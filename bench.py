@@ -298,6 +298,10 @@ def validation_latency() -> dict:
         out["pow_hash_block_call_us_p90"] = g["call_us_p90"]
         out["pow_hash_block_kernel_us_median"] = g["kernel_us_median"]
         out["calls"] = g["calls"]
+        from mpi_blockchain_amd.miner import GpuMiner
+
+        with GpuMiner(0) as m:  # how K2' is launched: "direct" (AQL packet, pow_aql.cpp) or "hip"
+            out["launch_path"] = m.launch_path()
     except Exception as e:  # pragma: no cover - reported, not fatal
         out["gpu_error"] = str(e)[-300:]
     try:
@@ -313,7 +317,7 @@ def validation_latency() -> dict:
     except Exception as e:  # pragma: no cover
         out["reference_error"] = str(e)[-300:]
     out["note"] = ("one block per call, as validate_block_for_chain checks a received block; GPU: call = "
-                   "launch + kernel + result in mapped host memory; reference: picosha2 + hex on one host core")
+                   "AQL packet (launch_path) + kernel + result in mapped host memory; reference: picosha2 + hex on one host core")
     return out
 
 
