@@ -278,3 +278,46 @@ def test_k2_one_block_is_the_rounds_only(isa):
     assert 4480 <= len(re.findall(r"^\s+v_", body, flags=re.M)) <= 4620
     assert len(re.findall(r"^\s+ds_read_b128", body, flags=re.M)) == 80
     assert len(re.findall(r"^\s+v_add3_u32", body, flags=re.M)) == 2 * 320
+
+
+AQL_KERNELS = ["_Z12pow_hash_one6PowMsgP10PowHashOutj"] + [
+    f"_Z14pow_search_latILb{f}ELb{a}ELb{g}EEv12PowConstsLat12PowLaunchLatP9PowResultS3_"
+    for g in (0, 1) for a in (0, 1) for f in (0, 1)]
+
+
+def test_direct_dispatch_kernels_take_explicit_args_only(isa):
+    """pow_aql.cpp writes exactly the kernels' explicit arguments into a packet's
+    kernarg slot (PowMsg + pointer + seq = 1,292 B; PowConstsLat + PowLaunchLat
+    + 2 pointers = 1,568 B) and nothing the HIP runtime would add: no kernel it
+    dispatches may read hidden arguments (gridDim, blockDim, printf buffer...)."""
+    for name in AQL_KERNELS:
+        blk = next(b for b in isa.split("  - .agpr_count")[1:] if re.search(rf"\.name:\s+{name}\s", b))
+        size = int(re.search(r"\.kernarg_segment_size:\s+(\d+)", blk).group(1))
+        assert size == (1292 if "hash_one" in name else 1568), (name, size)
+        assert "hidden_" not in blk, name
+
+
+def test_library_embeds_its_code_object():
+    """pow_aql.cpp loads the kernels from the gfx950 code object in the offload
+    bundle of its own .so file: both libraries hold one that names every kernel
+    it dispatches (the same scan as own_code_object)."""
+    from mpi_blockchain_amd import _lib
+
+    for path in (_lib.LIB_PATH, _lib.TEST_LIB_PATH):
+        data = open(path, "rb").read()
+        found = None
+        i = data.find(b"__CLANG_OFFLOAD_BUNDLE__")
+        while i >= 0 and found is None:
+            n = int.from_bytes(data[i + 24:i + 32], "little")
+            off = i + 32
+            for _ in range(min(n, 16)):
+                o, sz, tl = (int.from_bytes(data[off + 8 * k:off + 8 * k + 8], "little") for k in range(3))
+                triple = data[off + 24:off + 24 + tl]
+                off += 24 + tl
+                co = data[i + o:i + o + sz]
+                if triple == b"hipv4-amdgcn-amd-amdhsa--gfx950" and b"_Z12pow_hash_one" in co:
+                    found = co
+            i = data.find(b"__CLANG_OFFLOAD_BUNDLE__", i + 1)
+        assert found is not None and found[:4] == b"\x7fELF", path
+        for name in AQL_KERNELS:
+            assert (name + ".kd").encode() in found, (path, name)
