@@ -1,6 +1,6 @@
 // Direct AQL dispatch of the one-block and latency kernels (K2' pow_hash_one,
-// K1' pow_search_lat): an HSA queue of the context's own, an AQL kernel-dispatch
-// packet written into it and its doorbell rung, instead of hipLaunchKernel.
+// K1' pow_search_lat): an AQL kernel-dispatch packet written into an HSA queue
+// of the library's own and its doorbell rung, instead of hipLaunchKernel.
 //
 // Why: these launches are latency-bound.  A block validation (pow_hash_block,
 // valid_new_block / validate_block_for_chain, node.cpp:199-253) is ~10 us of
@@ -26,9 +26,13 @@
 //    arguments are uncached, the result words (PowResult) are written by the
 //    previous launch on this device, and host-memory words (cancel epoch, stop
 //    board) are read with system-scope atomics in the kernels;
-//  * release fence at system scope, barrier bit (launches on one queue run in
-//    order), and a completion signal counting launches in flight, so a launch
-//    that ends without publishing its result is still seen.
+//  * release fence at system scope, and a completion signal per context that
+//    counts its launches in flight, so a launch that ends without publishing
+//    its result is still seen;
+//  * one queue per device and process (pow_aql_open), packets without the
+//    barrier bit: each context orders its own launches by waiting for each
+//    one's result, and one context's validation does not wait behind
+//    another's running search.
 // Any failure to set this up leaves the caller on the HIP launch path (the
 // same kernels).
 #include <dlfcn.h>
@@ -51,7 +55,8 @@
 
 namespace {
 
-constexpr uint32_t kQueueSize = 64;    // packets; launches are host-waited, so one is ever in flight
+constexpr uint32_t kQueueSize = 64;         // argument slots per context (and packets of an own queue)
+constexpr uint32_t kSharedQueueSize = 256;  // packets of the device's shared queue
 constexpr uint32_t kSlotBytes = 2048;  // kernel-argument slot (largest: K1', 1,568 B)
 constexpr int kMaxDevices = 64;
 
@@ -87,6 +92,10 @@ struct DeviceKernels {
     uint64_t object = 0;
     uint32_t kernarg = 0, group = 0, priv = 0;
   } k[POW_AQL_NKERNELS];
+  // The device's dispatch queue, shared by every context of the process
+  // (created at the first pow_aql_open, kept for the process's lifetime)
+  hsa_queue_t* queue = nullptr;
+  std::atomic<int> queue_error{0};
 };
 
 std::mutex g_mu;
@@ -171,7 +180,7 @@ bool own_code_object(std::vector<char>& out, std::string& why) {
 }
 
 // Load (once) the kernels for `device`; the caller holds g_mu.
-const DeviceKernels* device_kernels(int device) {
+DeviceKernels* device_kernels(int device) {
   DeviceKernels& D = g_dev[device];
   if (D.tried) return &D;
   D.tried = true;
@@ -229,17 +238,20 @@ const DeviceKernels* device_kernels(int device) {
 struct pow_aql {
   const DeviceKernels* dk = nullptr;
   unsigned flags = 0;        // POW_AQL_EXP_* (test library experiments)
-  hsa_queue_t* q = nullptr;
-  hsa_signal_t done{};       // completion signal: the number of launches in flight
+  hsa_queue_t* q = nullptr;  // the device's shared queue, or (POW_AQL_EXP_OWN_QUEUE) this context's own
+  bool own_q = false;
+  std::atomic<int> own_error{0};
+  std::atomic<int>* queue_error = nullptr;  // set by the queue's error callback
+  hsa_signal_t done{};       // completion signal: this context's launches in flight
   bool signal_up = false;
   uint8_t* ring = nullptr;   // kernel-argument slots: device memory the host writes
   int ring_kind = 0;         // 1 host memory, 2 device memory
-  std::atomic<int> queue_error{0};
+  uint32_t next_slot = 0;    // this context's launches so far (ring slot = next_slot % kQueueSize)
 };
 
 namespace {
 void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
-  static_cast<pow_aql*>(data)->queue_error.store((int)st, std::memory_order_release);
+  static_cast<std::atomic<int>*>(data)->store((int)st, std::memory_order_release);
 }
 }  // namespace
 
@@ -249,18 +261,36 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
     if (why) *why = "device index";
     return -1;
   }
-  const DeviceKernels* dk;
+  // One queue per device and process, shared by its contexts: a pow_node rank
+  // has two (mining, validation), and a network of ranks on one GPU would
+  // otherwise hold two user-mode queues per rank beside HIP's own.  Packets
+  // carry no barrier bit, so a validation is not held behind a running
+  // latency search of another context: each context orders its own launches
+  // by waiting for each one's result.
+  DeviceKernels* dk;
+  hsa_queue_t* shared = nullptr;
   {
     std::lock_guard<std::mutex> g(g_mu);
     dk = device_kernels(device);
+    if (dk->ok && !dk->queue && !(flags & POW_AQL_EXP_OWN_QUEUE) &&
+        hsa_queue_create(dk->agent, kSharedQueueSize, HSA_QUEUE_TYPE_MULTI, on_queue_error, &dk->queue_error,
+                         UINT32_MAX, UINT32_MAX, &dk->queue) != HSA_STATUS_SUCCESS)
+      dk->queue = nullptr;
+    shared = dk->queue;
   }
   if (!dk->ok) {
     if (why) *why = dk->why;
     return -1;
   }
+  if (!shared && !(flags & POW_AQL_EXP_OWN_QUEUE)) {
+    if (why) *why = "hsa_queue_create";
+    return -1;
+  }
   pow_aql* a = new pow_aql;
   a->dk = dk;
   a->flags = flags;
+  a->q = shared;
+  a->queue_error = &dk->queue_error;
   auto bail = [&](const char* w) {
     if (why) *why = w;
     pow_aql_close(a);
@@ -287,31 +317,36 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
       hsa_signal_create(0, 0, nullptr, &a->done) != HSA_STATUS_SUCCESS)
     return bail("completion signal");
   a->signal_up = true;
-  if (hsa_queue_create(dk->agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a, UINT32_MAX, UINT32_MAX,
-                       &a->q) != HSA_STATUS_SUCCESS)
-    return bail("hsa_queue_create");
+  if (flags & POW_AQL_EXP_OWN_QUEUE) {
+    a->queue_error = &a->own_error;
+    if (hsa_queue_create(dk->agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, &a->own_error, UINT32_MAX,
+                         UINT32_MAX, &a->q) != HSA_STATUS_SUCCESS) {
+      a->q = nullptr;
+      return bail("hsa_queue_create");
+    }
+    a->own_q = true;
+  }
   *out = a;
   return 0;
 }
 
 void pow_aql_close(pow_aql* a) {
   if (!a) return;
-  if (a->q) {
-    // Launches are host-waited, so the queue is idle here unless one failed
-    // mid-flight: wait (bounded) for the last one to complete.
-    for (int n = 0; n < 1000000 && a->signal_up && hsa_signal_load_scacquire(a->done) != 0 &&
-                    !a->queue_error.load(std::memory_order_acquire);
-         ++n)
-      usleep(1);
-    hsa_queue_destroy(a->q);
-  }
+  // Launches are host-waited, so none of this context's is in flight unless
+  // one failed mid-flight: wait (bounded) for the last one to complete before
+  // its argument ring and signal go.
+  for (int n = 0; n < 1000000 && a->signal_up && a->q && hsa_signal_load_scacquire(a->done) != 0 &&
+                  !a->queue_error->load(std::memory_order_acquire);
+       ++n)
+    usleep(1);
+  if (a->own_q) hsa_queue_destroy(a->q);
   if (a->signal_up) hsa_signal_destroy(a->done);
   if (a->ring) (void)(a->ring_kind == 1 ? hipHostFree(a->ring) : hipFree(a->ring));
   delete a;
 }
 
 int pow_aql_status(const pow_aql* a) {
-  const int e = a->queue_error.load(std::memory_order_acquire);
+  const int e = a->queue_error->load(std::memory_order_acquire);
   if (e) return -e;
   if (a->flags & POW_AQL_EXP_NO_SIGNAL) return 1;
   return hsa_signal_load_scacquire(a->done) == 0 ? 0 : 1;
@@ -323,14 +358,11 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
       (uint64_t)workgroups * wg_size > 0xFFFFFFFFull)
     return -1;
   const DeviceKernels::Kern& K = a->dk->k[kernel];
-  if (nbytes != K.kernarg || a->queue_error.load(std::memory_order_acquire)) return -1;
+  if (nbytes != K.kernarg || a->queue_error->load(std::memory_order_acquire)) return -1;
   hsa_queue_t* q = a->q;
-  const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
-  // The slot is free once the packet processor has read past idx - size
-  // (launches are host-waited, so this never waits in practice).
-  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size)
-    if (a->queue_error.load(std::memory_order_acquire)) return -1;
-  uint8_t* arg = a->ring + (size_t)kSlotBytes * (idx % q->size);
+  // This context's argument slot: its launches are host-waited, so the slot's
+  // previous user (kQueueSize launches ago) has finished reading it.
+  uint8_t* arg = a->ring + (size_t)kSlotBytes * (a->next_slot++ % kQueueSize);
   memcpy(arg, args, nbytes);
   // Device memory written over PCIe: drain the write-combining buffers, flush
   // the HDP, and read a word back, so the kernel reads the new arguments.
@@ -350,6 +382,11 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
   // and started the next launch: a count, not a flag)
   const bool sig = !(a->flags & POW_AQL_EXP_NO_SIGNAL);
   if (sig) hsa_signal_add_scacq_screl(a->done, 1);
+  // The packet slot is free once the packet processor has read past
+  // idx - size (at most a few packets are ever outstanding).
+  const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
+  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size)
+    if (a->queue_error->load(std::memory_order_acquire)) return -1;
   hsa_kernel_dispatch_packet_t* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx % q->size);
   memset((uint8_t*)pk + 4, 0, sizeof *pk - 4);  // everything but header + setup, which go last
   pk->workgroup_size_x = (uint16_t)wg_size;
@@ -364,7 +401,7 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
   pk->kernarg_address = arg;
   if (sig) pk->completion_signal = a->done;
   const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                     ((a->flags & POW_AQL_EXP_NO_BARRIER) ? 0 : (1 << HSA_PACKET_HEADER_BARRIER)) |
+                                     (a->own_q ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
                                      (((a->flags & POW_AQL_EXP_ACQUIRE_SYSTEM) ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT)
                                       << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                      (((a->flags & POW_AQL_EXP_RELEASE_AGENT) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM)

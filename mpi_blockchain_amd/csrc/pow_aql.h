@@ -13,8 +13,8 @@ enum {
   POW_AQL_NKERNELS = 9
 };
 
-// A queue of its own on `device` (the kernels are loaded once per device per
-// process).  0 = ready; -1 = not available here (*why says why; the caller
+// A dispatcher for one context on `device` (the kernels and the queue are
+// shared by the process's contexts on the device).  0 = ready; -1 = not available here (*why says why; the caller
 // keeps the HIP launch path).
 int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why);
 // Dispatch experiments (flags of pow_aql_open; the shipped library passes 0,
@@ -24,7 +24,7 @@ enum {
   POW_AQL_EXP_NO_FLUSH = 2,     // no HDP flush / read-back after writing the arguments
   POW_AQL_EXP_NO_READBACK = 4,  // HDP flush, no read-back
   POW_AQL_EXP_HOST_ARGS = 8,    // arguments in coherent host memory instead of device memory
-  POW_AQL_EXP_NO_BARRIER = 16,  // packets without the barrier bit
+  POW_AQL_EXP_OWN_QUEUE = 16,   // a queue of the context's own (packets with the barrier bit)
   POW_AQL_EXP_READBACK_ONLY = 32,  // no HDP flush: re-store the last word, mfence, read it back
   POW_AQL_EXP_FINE_ARGS = 64,   // arguments in fine-grained device memory (cached in L2)
   POW_AQL_EXP_ACQUIRE_SYSTEM = 128,  // packet acquire fence at system scope (L2 invalidate)

@@ -12,6 +12,7 @@ The loop stops at the first failed run (no retries): its output is printed.
     python tools/protocol_soak.py --runs 40 --ranks 8 --difficulty 5
     python tools/protocol_soak.py --runs 40 --ranks 8 --difficulty 5 --forced-fork
     python tools/protocol_soak.py --runs 20 --ranks 2 --ref 2 --difficulty 9   # mixed networks
+    python tools/protocol_soak.py --runs 20 --ranks 4 --difficulty 9 --mutual     # mutual chain requests
 
 With --ref K the job also holds K ranks of the REFERENCE's own binary
 (oracle/_ref/blockchain_ref, whose difficulty is its macro, 9), as in
@@ -42,8 +43,13 @@ def main() -> int:
     ap.add_argument("--forced-fork", action="store_true",
                     help="--hold-first 1 instead of the timing knobs: every rank mines its own block 1 and "
                          "publishes it after a barrier, so every run must show rival blocks")
+    ap.add_argument("--mutual", action="store_true",
+                    help="--private-lead 3, as tests/test_node_gpu.py::test_mutual_chain_request: every rank "
+                         "must lose by several blocks and splice a peer's chain (find = 2)")
     a = ap.parse_args()
     extra = ("--hold-first", "1") if a.forced_fork else ("--winner-pause-us", "400", "--pause-us", "200")
+    if a.mutual:
+        extra = ("--private-lead", "3")
     ref = dict(ref_binary=os.path.join(ROOT, "oracle", "_ref", "blockchain_ref"), n_ref=a.ref) if a.ref else {}
     if a.ref:
         if a.difficulty != 9:
@@ -69,6 +75,9 @@ def main() -> int:
         n_fork = sum(run.stdout.count(m) for m in FORK_MSGS)
         if a.forced_fork:
             ok = ok and n_fork >= 1
+        if a.mutual:
+            ok = ok and all(f"[{r}] Perdí la carrera por varios contra" in run.stdout and
+                            f"[{r}]: find = 2 | received_blockchain_checks = 1" in run.stdout for r in range(a.ranks))
         cross = ""
         if a.ref:  # blocks adopted across implementations (reference ranks are 0..ref-1)
             acc = [(int(r), int(s_)) for r, s_ in
