@@ -45,6 +45,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -80,9 +81,8 @@ static_assert(sizeof(PowMsg) % 8 == 0 && sizeof(PowConstsLat) % 8 == 0 && sizeof
               "argument offsets");
 static_assert(kLatArgs <= kSlotBytes && kHashArgs <= kSlotBytes, "slot size");
 
-// The kernels of one device, loaded once per process and kept for its
-// lifetime (an executable torn down beside the HIP runtime's own exit path
-// gains nothing).
+// The kernels of one device, loaded once per process and released at its
+// exit (release_all), before the HIP runtime's own teardown.
 struct DeviceKernels {
   bool tried = false, ok = false;
   std::string why;
@@ -96,10 +96,32 @@ struct DeviceKernels {
   // (created at the first pow_aql_open, kept for the process's lifetime)
   hsa_queue_t* queue = nullptr;
   std::atomic<int> queue_error{0};
+  bool hsa_up = false, reader_up = false, exe_up = false;
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  std::vector<char> code;  // the code object the reader was made from
 };
 
 std::mutex g_mu;
 DeviceKernels g_dev[kMaxDevices];
+bool g_atexit = false;
+
+// At process exit: the shared queues, the executables and this library's
+// reference on the HSA runtime (hsa_init is reference-counted), so the
+// runtime's own teardown (HIP's, registered before this one, so it runs after
+// it) finds nothing of ours and joins its threads.  Contexts still open at
+// exit have no launch in flight (every launch is host-waited).
+void release_all() {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (DeviceKernels& D : g_dev) {
+    if (D.queue) hsa_queue_destroy(D.queue);
+    if (D.exe_up) hsa_executable_destroy(D.exe);
+    if (D.reader_up) hsa_code_object_reader_destroy(D.reader);
+    if (D.hsa_up) hsa_shut_down();
+    D.queue = nullptr;
+    D.ok = D.exe_up = D.reader_up = D.hsa_up = false;
+  }
+}
 
 struct AgentSearch {
   uint32_t bus, dev, domain;
@@ -191,25 +213,26 @@ DeviceKernels* device_kernels(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail("hipGetDeviceProperties");
   if (hsa_init() != HSA_STATUS_SUCCESS) return bail("hsa_init");  // reference-counted; the HIP runtime holds one
+  D.hsa_up = true;
+  if (!g_atexit) g_atexit = atexit(release_all) == 0;
   AgentSearch s{(uint32_t)prop.pciBusID, (uint32_t)prop.pciDeviceID, (uint32_t)prop.pciDomainID};
   if (hsa_iterate_agents(match_agent, &s) != HSA_STATUS_SUCCESS || !s.ok) return bail("no HSA agent for the device");
   D.agent = s.found;
-  std::vector<char>* code = new std::vector<char>;  // kept: the reader may refer to it
-  if (!own_code_object(*code, D.why)) return bail(D.why);
-  hsa_code_object_reader_t reader;
-  hsa_executable_t exe;
-  if (hsa_code_object_reader_create_from_memory(code->data(), code->size(), &reader) != HSA_STATUS_SUCCESS)
+  if (!own_code_object(D.code, D.why)) return bail(D.why);
+  if (hsa_code_object_reader_create_from_memory(D.code.data(), D.code.size(), &D.reader) != HSA_STATUS_SUCCESS)
     return bail("hsa_code_object_reader_create_from_memory");
-  if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe) !=
+  D.reader_up = true;
+  if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &D.exe) !=
       HSA_STATUS_SUCCESS)
     return bail("hsa_executable_create_alt");
-  if (hsa_executable_load_agent_code_object(exe, D.agent, reader, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
-      hsa_executable_freeze(exe, nullptr) != HSA_STATUS_SUCCESS)
+  D.exe_up = true;
+  if (hsa_executable_load_agent_code_object(D.exe, D.agent, D.reader, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+      hsa_executable_freeze(D.exe, nullptr) != HSA_STATUS_SUCCESS)
     return bail("loading the code object");
   for (int i = 0; i < POW_AQL_NKERNELS; ++i) {
     hsa_executable_symbol_t sym;
     DeviceKernels::Kern& K = D.k[i];
-    if (hsa_executable_get_symbol_by_name(exe, kNames[i], &D.agent, &sym) != HSA_STATUS_SUCCESS ||
+    if (hsa_executable_get_symbol_by_name(D.exe, kNames[i], &D.agent, &sym) != HSA_STATUS_SUCCESS ||
         hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &K.object) !=
             HSA_STATUS_SUCCESS ||
         hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &K.kernarg) !=
