@@ -397,7 +397,8 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
     (void)*(volatile uint32_t*)(arg + nbytes - 4);
     __builtin_ia32_lfence();
   } else if (!(a->flags & (POW_AQL_EXP_NO_FLUSH | POW_AQL_EXP_HOST_ARGS))) {
-    *(volatile uint32_t*)a->dk->hdp_flush = 1u;
+    // (a register every context of the process writes: an atomic store)
+    __atomic_store_n((volatile uint32_t*)a->dk->hdp_flush, 1u, __ATOMIC_RELAXED);
     if (!(a->flags & POW_AQL_EXP_NO_READBACK)) (void)*(volatile uint32_t*)(arg + nbytes - 4);
   }
   // in flight += 1; the packet processor subtracts 1 when the launch
