@@ -664,11 +664,18 @@ __global__ __launch_bounds__(256) void pow_search_lat(
   for (unsigned long long qq = (unsigned long long)wave * 64u; qq < L.count;
        qq += (unsigned long long)nwaves * 64u) {
     const uint32_t q = (uint32_t)qq;
-    unsigned long long f =
-        __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    f = uniform64(f);
-    if (ANY ? f != ~0ull : f < (unsigned long long)q) break;
-    if (poll_stop(L.watch, &res->cancelled, &res->peer_abs, ANY ? ~0ull : L.watch.abs_start + q)) break;
+    // The stop checks wait for device (and, for the sentinel wave, host)
+    // memory before the trial can start: skipped in a wave's first iteration,
+    // where no hit of this launch can exist yet and a cancel or a peer's hit
+    // is seen one trial later.  At d <= 13 most launches are that one
+    // iteration, and those round trips were on the time-to-block's path.
+    if (iters != 0) {
+      unsigned long long f =
+          __hip_atomic_load(&res->min_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      f = uniform64(f);
+      if (ANY ? f != ~0ull : f < (unsigned long long)q) break;
+      if (poll_stop(L.watch, &res->cancelled, &res->peer_abs, ANY ? ~0ull : L.watch.abs_start + q)) break;
+    }
     ++iters;
     const uint32_t rel = q + lane;
     uint32_t dg[9];
