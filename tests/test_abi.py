@@ -115,6 +115,7 @@ def test_null_arguments_rejected():
     n = ctypes.c_size_t()
     assert L.pow_sweep(None, ctypes.byref(b), 0, 1, 9, None, 0, ctypes.byref(n)) == _lib.POW_EINVAL
     assert L.pow_nonce_from_counter(0, None) == _lib.POW_EINVAL
+    assert L.pow_launch_path(None) == _lib.POW_EINVAL
 
 
 def test_sweep_cap_limit():
