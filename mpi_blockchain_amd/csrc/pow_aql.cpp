@@ -58,7 +58,7 @@ namespace {
 
 constexpr uint32_t kQueueSize = 64;         // argument slots per context (and packets of an own queue)
 constexpr uint32_t kSharedQueueSize = 256;  // packets of the device's shared queue
-constexpr uint32_t kSlotBytes = 2048;  // kernel-argument slot (largest: K1', 1,568 B)
+constexpr uint32_t kSlotBytes = 2048;       // kernel-argument slot (largest: K1', 1,568 B)
 constexpr int kMaxDevices = 64;
 
 const char* kNames[POW_AQL_NKERNELS] = {
@@ -93,7 +93,7 @@ struct DeviceKernels {
     uint32_t kernarg = 0, group = 0, priv = 0;
   } k[POW_AQL_NKERNELS];
   // The device's dispatch queue, shared by every context of the process
-  // (created at the first pow_aql_open, kept for the process's lifetime)
+  // (created at the first pow_aql_open, destroyed by release_all at exit)
   hsa_queue_t* queue = nullptr;
   std::atomic<int> queue_error{0};
   bool hsa_up = false, reader_up = false, exe_up = false;
