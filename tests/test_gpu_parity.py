@@ -336,6 +336,49 @@ def test_validation_beside_mining():
         assert statistics.median(lat) < 0.005, lat
 
 
+def test_direct_dispatch_two_threads(golden, templates):
+    """Two contexts of one process driven from two threads at once, as in a
+    pow_node rank (miner thread: pow_mine_any on K1', receive thread:
+    pow_hash_block on K2'): both put packets into the process's one dispatch
+    queue (pow_aql.cpp, no barrier bit).  Every result must stay exact: the
+    lowest solutions of the golden window and the reference's digests."""
+    import threading
+
+    w = golden["windows"][0]
+    tmpl = block_from_template(templates[w["template"]])
+    firsts = {int(d): w["start"] + st["counters"][0] for d, st in w["sets"].items() if st["count"]}
+    blocks = [block_from_random(e) for e in golden["random_blocks"]]
+    want = [e["hex"] for e in golden["random_blocks"]]
+    errors = []
+    with GpuMiner(0) as m, GpuMiner(0) as v:
+        assert m.launch_path() == v.launch_path() == "direct"
+
+        def mine_loop():
+            try:
+                for _ in range(60):
+                    for d, first in firsts.items():
+                        if d <= 13:
+                            r = m.mine(tmpl, w["start"], w["count"], d)
+                            if r is None or r.counter != first:
+                                errors.append(("mine", d, r and r.counter, first))
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(("mine", repr(e)))
+
+        th = threading.Thread(target=mine_loop)
+        th.start()
+        n = 0
+        while th.is_alive() and n < 20000:
+            for b, hx in zip(blocks, want):
+                got = v.block_to_hash(b)
+                if got != hx:
+                    errors.append(("hash", got, hx))
+                n += 1
+        th.join(timeout=60)
+        assert not th.is_alive()
+    assert not errors, errors[:5]
+    assert n >= len(blocks)
+
+
 def test_chained_blocks_validate(miner):
     """Mine three chained blocks with the GPU and check the chain the way the
     receive side does (valid_new_block, block.cpp:13-25: recomputed hash ==
