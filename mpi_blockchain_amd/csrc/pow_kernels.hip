@@ -795,8 +795,12 @@ __global__ __launch_bounds__(256) void pow_search_lat(
         res->cancelled = 0;
         res->peer_abs = ~0ull;
       }
-      __threadfence_system();
-      if (lane == 0) __hip_atomic_store(&hout->done, L.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      // Release at system scope, then `done`: the result words above (host
+      // memory) and the reset of `res` are visible before the host sees this
+      // launch's seq.  A release fence, not __threadfence_system: its acquire
+      // half invalidated the whole L2 again at the end of every launch.
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (lane == 0) __hip_atomic_store(&hout->done, L.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
