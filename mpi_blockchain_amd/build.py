@@ -17,7 +17,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libpow_gpu.so")
-SOURCES = ["pow_api.cpp", "pow_aql.cpp", "pow_board.cpp", "pow_group.cpp", "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip"]
+SOURCES = ["pow_api.cpp", "pow_aql.cpp", "pow_board.cpp", "pow_group.cpp", "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip",
+           "pow_test_kernels.hip"]
 HEADERS = ["pow_template.h", "sha256_dev.h", "pow_aql.h"]
 INCLUDES = [os.path.join(ROOT, "include", h) for h in ("pow_gpu.h", "pow_tools.h")]
 ARCH = "gfx950"
@@ -42,6 +43,10 @@ def _inputs() -> list[str]:
 TEST_LIB = os.path.join(PKG, "libpow_gpu_test.so")
 OBJ = os.path.join(ROOT, "build", "obj")  # git- and gpurun-ignored: the .so files travel, not the objects
 HOOKED = ("pow_api.cpp", "pow_group.cpp")  # the sources that differ between the two builds
+# Direct AQL dispatch (round 4's K1'/K2' launch path): linked into the test
+# library only, opt-in there with POW_AQL=1.  The shipped library launches
+# every kernel through hipLaunchKernel and does not link the HSA runtime.
+TEST_ONLY = ("pow_aql.cpp", "pow_test_kernels.hip")  # + the watchdog tests' stall kernel
 
 
 def _flags() -> list[str]:
@@ -79,7 +84,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     common, plain, hooked = [], [], []
     for s in SOURCES:
         base = os.path.splitext(s)[0]
-        if s in HOOKED:
+        if s in TEST_ONLY:
+            hooked.append(os.path.join(OBJ, base + ".test.o"))
+            _compile(s, hooked[-1], ("-DPOW_TEST_HOOKS",), verbose)
+        elif s in HOOKED:
             plain.append(os.path.join(OBJ, base + ".o"))
             hooked.append(os.path.join(OBJ, base + ".test.o"))
             _compile(s, plain[-1], (), verbose)
@@ -88,8 +96,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
             common.append(os.path.join(OBJ, base + ".o"))
             _compile(s, common[-1], (), verbose)
     for lib, objs in ((LIB, plain), (TEST_LIB, hooked)):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *common, *objs, "-o", lib + ".tmp",
-               "-L", "/opt/rocm/lib", "-lhsa-runtime64", "-Wl,-rpath,/opt/rocm/lib"]  # pow_aql.cpp: direct dispatch
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *common, *objs, "-o", lib + ".tmp"]
+        if lib == TEST_LIB:  # pow_aql.cpp: direct dispatch
+            cmd += ["-L", "/opt/rocm/lib", "-lhsa-runtime64", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=ROOT)

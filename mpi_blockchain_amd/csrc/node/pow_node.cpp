@@ -184,6 +184,7 @@ class Node {
 #ifdef POW_NODE_TEST_KNOBS
   std::atomic<int> rivals1_{0};  // --hold-first: peers' blocks 1 this rank has processed
   MPI_Comm test_comm_ = MPI_COMM_NULL;  // --private-lead: the receive thread's own barrier
+  MPI_Comm lead_comm_ = MPI_COMM_NULL;  // --private-lead: the miners' barrier after every migration
   bool tip_seen_ = false;               // --private-lead: a peer's private tip has arrived
 #endif
 
@@ -405,7 +406,14 @@ class Node {
   // the mutex, so every rank's tip goes out at once.  Each receiver is K
   // behind ("Perdí la carrera por varios", node.cpp:249-253) and asks the
   // tip's owner for its chain while that owner asks it.  Then wait (bounded)
-  // until this rank has migrated, so no block 1 is mined on genesis meanwhile.
+  // until this rank has migrated, so no block 1 is mined on genesis meanwhile,
+  // and then for every other rank's miner to have done the same (lead_comm_):
+  // without that, the first ranks to migrate mine blocks 4..10 in a few ms and
+  // the finisher's MPI_Abort (node.cpp:330) can end the job before a slower
+  // rank has logged its own migration (the test then sees a rank that "logged
+  // nothing" after its tip: a termination race, not a hang).  The bound (30 s)
+  // is longer than the launch watchdog (10 s), so a launch that never
+  // completes aborts the job with its diagnostic before the bound expires.
   void private_lead(std::mt19937_64& rng, uint64_t round) {
     pow_block prev;
     {
@@ -437,13 +445,19 @@ class Node {
     }
     MPI_Barrier(MPI_COMM_WORLD);
     send_block_to_everyone(prev);
-    for (int w = 0; w < 40000; ++w) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (bool migrated = false; !migrated;) {
       {
         std::lock_guard<std::mutex> g(mu_);
-        if (last_->index >= opt_.t.private_lead) break;
+        migrated = last_->index >= opt_.t.private_lead;
       }
-      std::this_thread::sleep_for(std::chrono::microseconds(50));
+      if (!migrated && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+        printf("[%d] private-lead: no migration after 30 s\n", rank_);
+        break;
+      }
+      if (!migrated) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+    MPI_Barrier(lead_comm_);
   }
 #endif
 
@@ -573,7 +587,10 @@ int Node::run() {
   MPI_Comm_rank(MPI_COMM_WORLD, &rank_);
   define_block_type();
 #ifdef POW_NODE_TEST_KNOBS
-  if (opt_.t.private_lead >= 2) MPI_Comm_dup(MPI_COMM_WORLD, &test_comm_);
+  if (opt_.t.private_lead >= 2) {
+    MPI_Comm_dup(MPI_COMM_WORLD, &test_comm_);
+    MPI_Comm_dup(MPI_COMM_WORLD, &lead_comm_);
+  }
 #endif
   printf("[MPI] Lanzando proceso %u\n", rank_);
   std::remove((std::to_string(rank_) + ".out").c_str());  // blockchain.cpp:31 does `rm *.out`

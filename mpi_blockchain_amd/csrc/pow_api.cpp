@@ -6,6 +6,7 @@
 // each entry point to the reference function it replaces.
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -19,8 +20,10 @@
 #include <vector>
 
 #include "../../include/pow_gpu.h"
-#include "pow_aql.h"
 #include "pow_template.h"
+#ifdef POW_TEST_HOOKS
+#include "pow_aql.h"  // direct dispatch: test library only (POW_AQL=1)
+#endif
 
 #ifndef POW_WAIT_POLL_US
 #define POW_WAIT_POLL_US 50  // long launches: host poll period (us) of the completion event
@@ -55,6 +58,9 @@ hipError_t pow_sort_u32(void* temp, size_t* temp_bytes, uint32_t* keys, uint32_t
                         uint32_t** sorted, hipStream_t stream);
 hipError_t pow_launch_search_lat(bool full, bool any, bool asm_groups, unsigned grid, hipStream_t stream,
                                  const PowConstsLat& C, const PowLaunchLat& L, PowResult* res, PowResult* hout);
+#ifdef POW_TEST_HOOKS
+hipError_t pow_launch_test_stall(hipStream_t stream, unsigned us, int realtime_khz);  // pow_test_kernels.hip
+#endif
 
 namespace {
 
@@ -68,6 +74,12 @@ int fail(int code, const char* fmt, ...) {
   va_end(ap);
   g_err = buf;
   return code;
+}
+
+uint64_t mono_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
 }
 
 #define HIP_OK(expr)                                                                       \
@@ -218,10 +230,17 @@ struct pow_ctx {
   uint64_t lat_max = 1ull << 24;  // first-sub-round cap for K1' (0 = K1 only)
   unsigned lat_wps = 0;           // K1' waves per SIMD at every d (0 = the plan)
   bool sentinel_idle = false;     // K1 mine launches: the sentinel wave takes no chunk (POW_LAUNCH_SENTINEL_IDLE)
-  // K1' and K2' launches: packets written into a queue of the context's own
-  // (pow_aql.cpp) instead of hipLaunchKernel; null = the HIP launch path.
+  unsigned test_stall_us = 0;     // POW_TEST_STALL_US: a bounded stall kernel in front of every HIP launch (watchdog tests)
+#ifdef POW_TEST_HOOKS
+  // K1' and K2' launches as AQL packets (pow_aql.cpp) instead of
+  // hipLaunchKernel: test library only, with POW_AQL=1; null = the HIP launch
+  // path, the only one the shipped library has.
   pow_aql* aql = nullptr;
   std::string aql_why;            // why aql is null, if it is
+#endif
+  // Watchdog (every host wait on a launch is bounded): base deadline of a
+  // latency launch, and of a throughput launch on top of its per-counter share.
+  uint64_t watchdog_ns = 10ull * 1000000000ull;
   pow_stats stats{};
 };
 
@@ -306,29 +325,50 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
 #endif
   if (int rc2 = stage_result(ctx, true, start)) return rc2;
   const unsigned grid = grid_for(ctx, L.n_prefix);
+#ifdef POW_TEST_HOOKS
+  if (ctx->test_stall_us) HIP_OK(pow_launch_test_stall(ctx->stream, ctx->test_stall_us, ctx->realtime_khz));
+#endif
   HIP_OK(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_OK(pow_launch_search((int)mode, diff > 32 || ctx->force_full, grid, ctx->stream, ctx->d_consts, L, dev_out,
                            ctx->d_res));
   HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
-  // Long launches (>= 2^26 counters, >= 8 ms): poll an event every 50 us
+  HIP_OK(hipEventRecord(ctx->ev_block, ctx->stream));
+  // The wait is bounded (watchdog): the base deadline plus 2 ns per counter,
+  // i.e. a launch slower than 0.5 G trials/s (1/18 of the chip's rate, e.g.
+  // one GPU shared by many processes) is reported as stuck instead of waited
+  // for forever.
+  // Long launches (>= 2^26 counters, >= 8 ms): poll the event every 50 us
   // instead of spinning a host core for the whole kernel (a
   // protocol rank should not burn a core while its GPU mines; hipEvent-
   // Synchronize spins, blocking-sync event or not).  At most 50 us late on a
-  // >= 8 ms launch.  Short launches keep the spin wait: their latency is the
-  // whole time-to-block at low difficulty.
+  // >= 8 ms launch.  Short launches spin: their latency is the whole
+  // time-to-block at low difficulty.
   // The calling thread's timer slack (50 us by default on Linux) is lowered
   // to 1 us for the wait: a 50 us sleep otherwise lasts ~100 us, and the end
   // of a pow_mine_any launch that found a block at d = 25 was seen 50-75 us
   // late (rocprofv3 HIP trace of tools/ttb_c 25).
-  if (count >= (1ull << 26)) {
-    HIP_OK(hipEventRecord(ctx->ev_block, ctx->stream));
-    const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+  {
+    const bool nap = count >= (1ull << 26);
+    const uint64_t t0 = mono_ns(), deadline = t0 + ctx->watchdog_ns + 2ull * count;
+    const int slack = nap ? prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0) : 0;
     if (slack > 1000) prctl(PR_SET_TIMERSLACK, 1000ul, 0, 0, 0);
     hipError_t q;
-    while ((q = hipEventQuery(ctx->ev_block)) == hipErrorNotReady)
-      std::this_thread::sleep_for(std::chrono::microseconds(POW_WAIT_POLL_US));
+    bool late = false;
+    for (uint32_t n = 1; (q = hipEventQuery(ctx->ev_block)) == hipErrorNotReady; ++n) {
+      if (nap) std::this_thread::sleep_for(std::chrono::microseconds(POW_WAIT_POLL_US));
+      if ((nap || (n & 255u) == 0) && mono_ns() > deadline) {
+        late = true;
+        break;
+      }
+    }
     if (slack > 1000) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+    if (late)
+      return fail(POW_EHIP,
+                  "search kernel (mode %u, %llu counters from %llu, d = %u): watchdog: not complete after %.3f s "
+                  "(deadline %.3f s; hipStreamQuery: %s); the context must not be reused",
+                  mode, (unsigned long long)count, (unsigned long long)start, diff, (mono_ns() - t0) * 1e-9,
+                  (deadline - t0) * 1e-9, hipGetErrorString(hipStreamQuery(ctx->stream)));
     HIP_OK(q);
   }
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -340,6 +380,7 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
   return POW_OK;
 }
 
+#ifdef POW_TEST_HOOKS
 // The explicit kernel arguments of a direct dispatch (pow_aql.cpp): the
 // parameters in declaration order, each at its natural alignment.
 struct ArgPack {
@@ -352,60 +393,113 @@ struct ArgPack {
     n += (uint32_t)sizeof v;
   }
 };
+#endif
 
 // Wait for a latency-bound launch to publish `seq` into its done word (mapped
 // host memory): return as soon as it shows, without waiting for the kernel's
 // completion signal (~5 us later; rocprofv3 trace of tools/ttb_c, DESIGN.md
 // §4).  A launch that ends without publishing (a fault, a queue error) is
-// caught by a completion check every 65536 polls (~60 us).
-int wait_published(pow_ctx* ctx, const volatile uint32_t* done, uint32_t seq, const char* what) {
+// caught by a completion check every 65536 polls (~60 us), and one that does
+// not end by `deadline_ns` (CLOCK_MONOTONIC) by the watchdog: POW_EHIP with
+// the launch's sequence number, the done word and the launch path's state
+// (HIP: the stream's status; direct dispatch: the completion signal, the
+// queue's indices and the header in the packet's slot).  The context must not
+// be reused after a watchdog error: its launch may still be queued.
+int wait_published(pow_ctx* ctx, const volatile uint32_t* done, uint32_t seq, const char* what,
+                   uint64_t t0, uint64_t deadline_ns) {
   for (uint32_t n = 1; __atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE) != seq; ++n) {
     if ((n & 0xFFFFu) != 0) continue;
     int st;  // 1 = running, 0 = ended, < 0 = error
     hipError_t q = hipSuccess;
+#ifdef POW_TEST_HOOKS
     if (ctx->aql) {
       st = pow_aql_status(ctx->aql);
-    } else {
+    } else
+#endif
+    {
       q = hipStreamQuery(ctx->stream);
       st = q == hipErrorNotReady ? 1 : q == hipSuccess ? 0 : -1;
     }
-    if (st == 1) continue;
+    if (st == 1) {
+      if (mono_ns() <= deadline_ns) continue;
+      const uint32_t seen = __atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE);
+      if (seen == seq) break;
+      std::string path = "launch path hip, hipStreamQuery: not ready";
+#ifdef POW_TEST_HOOKS
+      if (ctx->aql) path = "launch path direct, " + pow_aql_diag(ctx->aql);
+#endif
+      return fail(POW_EHIP, "%s: watchdog: no result after %.3f s (seq %u, done word %u; %s); the context must not be reused",
+                  what, (mono_ns() - t0) * 1e-9, seq, seen, path.c_str());
+    }
     if (__atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE) == seq) break;
+#ifdef POW_TEST_HOOKS
     if (st < 0 && ctx->aql) return fail(POW_EHIP, "%s: the dispatch queue reported HSA status 0x%x", what, -st);
+#endif
     HIP_OK(q);
-    return fail(POW_EHIP, "%s ended without publishing its result", what);
+    return fail(POW_EHIP, "%s ended without publishing its result (seq %u, done word %u)", what, seq,
+                __atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE));
   }
   return POW_OK;
 }
 
-int launch_hash_one(pow_ctx* ctx, const PowMsg& M, uint32_t seq) {
-  if (!ctx->aql) {
-    HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, seq));
+#ifdef POW_TEST_HOOKS
+// A context whose direct-dispatch queue has reported an error goes back to
+// the HIP launch path for good (pow_launch_path then says so).
+bool aql_usable(pow_ctx* ctx) {
+  if (!ctx->aql) return false;
+  if (pow_aql_status(ctx->aql) >= 0) return true;
+  ctx->aql_why = "the dispatch queue reported an error; back on the HIP launch path";
+#ifdef POW_TEST_HOOKS
+  pow_aql_close(ctx->aql);
+#endif
+  ctx->aql = nullptr;
+  return false;
+}
+#endif
+
+int launch_hash_one(pow_ctx* ctx, const PowMsg& M, uint32_t seq, uint64_t deadline_ns) {
+#ifdef POW_TEST_HOOKS
+  if (aql_usable(ctx)) {
+    ArgPack a;
+    a.put(M);
+    a.put(ctx->d_one);
+    a.put(seq);
+    std::string why;
+    if (pow_aql_dispatch(ctx->aql, POW_AQL_HASH_ONE, 1, 64, a.b, a.n, deadline_ns, &why))
+      return fail(POW_EHIP, "dispatch of pow_hash_one failed: %s (%s)", why.c_str(), pow_aql_diag(ctx->aql).c_str());
     return POW_OK;
   }
-  ArgPack a;
-  a.put(M);
-  a.put(ctx->d_one);
-  a.put(seq);
-  if (pow_aql_dispatch(ctx->aql, POW_AQL_HASH_ONE, 1, 64, a.b, a.n))
-    return fail(POW_EHIP, "dispatch of pow_hash_one failed (queue error 0x%x)", -pow_aql_status(ctx->aql));
+#endif
+  (void)deadline_ns;
+#ifdef POW_TEST_HOOKS
+  if (ctx->test_stall_us) HIP_OK(pow_launch_test_stall(ctx->stream, ctx->test_stall_us, ctx->realtime_khz));
+#endif
+  HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, seq));
   return POW_OK;
 }
 
-int launch_search_lat(pow_ctx* ctx, bool full, bool any, bool asm_groups, unsigned grid, const PowLaunchLat& L) {
-  if (!ctx->aql) {
-    HIP_OK(pow_launch_search_lat(full, any, asm_groups, grid, ctx->stream, ctx->lat_consts, L, ctx->d_lat,
-                                 ctx->d_lat_host));
+int launch_search_lat(pow_ctx* ctx, bool full, bool any, bool asm_groups, unsigned grid, const PowLaunchLat& L,
+                      uint64_t deadline_ns) {
+#ifdef POW_TEST_HOOKS
+  if (aql_usable(ctx)) {
+    ArgPack a;
+    a.put(ctx->lat_consts);
+    a.put(L);
+    a.put(ctx->d_lat);
+    a.put(ctx->d_lat_host);
+    const int k = POW_AQL_LAT0 + (full ? 1 : 0) + (any ? 2 : 0) + (asm_groups ? 4 : 0);
+    std::string why;
+    if (pow_aql_dispatch(ctx->aql, k, grid, 256, a.b, a.n, deadline_ns, &why))
+      return fail(POW_EHIP, "dispatch of pow_search_lat failed: %s (%s)", why.c_str(), pow_aql_diag(ctx->aql).c_str());
     return POW_OK;
   }
-  ArgPack a;
-  a.put(ctx->lat_consts);
-  a.put(L);
-  a.put(ctx->d_lat);
-  a.put(ctx->d_lat_host);
-  const int k = POW_AQL_LAT0 + (full ? 1 : 0) + (any ? 2 : 0) + (asm_groups ? 4 : 0);
-  if (pow_aql_dispatch(ctx->aql, k, grid, 256, a.b, a.n))
-    return fail(POW_EHIP, "dispatch of pow_search_lat failed (queue error 0x%x)", -pow_aql_status(ctx->aql));
+#endif
+  (void)deadline_ns;
+#ifdef POW_TEST_HOOKS
+  if (ctx->test_stall_us) HIP_OK(pow_launch_test_stall(ctx->stream, ctx->test_stall_us, ctx->realtime_khz));
+#endif
+  HIP_OK(pow_launch_search_lat(full, any, asm_groups, grid, ctx->stream, ctx->lat_consts, L, ctx->d_lat,
+                               ctx->d_lat_host));
   return POW_OK;
 }
 
@@ -436,8 +530,11 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   // trials/s, time-to-block 0.2136 -> 0.2125 ms (profiles/r03/ab/ab14_*).  At 1-2 waves per SIMD the kernel is latency-bound and the
   // compiler's interleaving of independent ops serves it better (d = 13:
   // 0.034 -> 0.038 ms with the groups; profiles/r03/ab/ab8_*).
-  if (int rc = launch_search_lat(ctx, diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, L)) return rc;
-  if (int rc = wait_published(ctx, &ctx->h_lat->done, L.seq, "latency kernel")) return rc;
+  // Watchdog: the base deadline plus 2 ns per counter (count <= 2^31).
+  const uint64_t t0 = mono_ns(), deadline = t0 + ctx->watchdog_ns + 2ull * count;
+  if (int rc = launch_search_lat(ctx, diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, L, deadline))
+    return rc;
+  if (int rc = wait_published(ctx, &ctx->h_lat->done, L.seq, "latency kernel", t0, deadline)) return rc;
   memcpy(ctx->h_res, (const void*)ctx->h_lat, sizeof(PowResult));
   const double ms = (double)ctx->h_res->ticks / ctx->realtime_khz;
   ctx->stats.kernel_ms += ms;
@@ -557,15 +654,17 @@ int pow_init(int device, pow_ctx** out) {
   if (const char* lm = getenv("POW_LAT_MAX")) ctx->lat_max = std::min<uint64_t>(strtoull(lm, nullptr, 0), 1ull << 31);
   if (const char* lw = getenv("POW_LAT_WPS")) ctx->lat_wps = (unsigned)std::min(8ul, strtoul(lw, nullptr, 0));
   if (const char* si = getenv("POW_TEST_SENTINEL_IDLE")) ctx->sentinel_idle = si[0] == '1';
+  if (const char* ts = getenv("POW_TEST_STALL_US")) ctx->test_stall_us = (unsigned)strtoul(ts, nullptr, 0);
   if (const char* g = getenv("POW_GRID_PER_CU")) {  // launch-geometry experiments
     const int per = atoi(g);
     if (per > 0 && per <= 64) ctx->grid_full = (unsigned)prop.multiProcessorCount * (unsigned)per;
   }
-  const char* no_aql = getenv("POW_NO_AQL");  // K1'/K2' through hipLaunchKernel (A/B, fallback tests)
+  // POW_AQL=1: K1'/K2' as AQL packets (pow_aql.cpp; dispatch A/B and the
+  // multi-producer ordering test), POW_AQL_EXP its experiment flags.
+  const char* use_aql = getenv("POW_AQL");
   const unsigned aql_flags = getenv("POW_AQL_EXP") ? (unsigned)strtoul(getenv("POW_AQL_EXP"), nullptr, 0) : 0u;
-#else
-  const char* no_aql = nullptr;
-  const unsigned aql_flags = 0;
+  // POW_WATCHDOG_MS: the watchdog's base deadline (tests of the watchdog itself)
+  if (const char* wd = getenv("POW_WATCHDOG_MS")) ctx->watchdog_ns = std::max(1ull, strtoull(wd, nullptr, 0)) * 1000000ull;
 #endif
   int rc = POW_OK;
   auto chk = [&](hipError_t e, const char* what) {
@@ -606,8 +705,10 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipHostMalloc(&ctx->h_res, sizeof(PowResult), hipHostMallocDefault), "hipHostMalloc");
   ctx->tail_cap = ctx->grid_full * 4u * 32u;  // < 32 per wave, 4 waves per workgroup
   chk(hipMalloc(&ctx->d_tail, (size_t)ctx->tail_cap * sizeof(uint32_t)), "hipMalloc sweep tail");
-  if (rc == POW_OK && !(no_aql && no_aql[0] == '1') && pow_aql_open(device, aql_flags, &ctx->aql, &ctx->aql_why) != 0)
-    ctx->aql = nullptr;  // the HIP launch path: same kernels, ~8 us more per launch
+#ifdef POW_TEST_HOOKS
+  if (rc == POW_OK && use_aql && use_aql[0] == '1' && pow_aql_open(device, aql_flags, &ctx->aql, &ctx->aql_why) != 0)
+    ctx->aql = nullptr;  // the HIP launch path
+#endif
   if (rc != POW_OK) {
     pow_destroy(ctx);
     return rc;
@@ -620,7 +721,9 @@ void pow_destroy(pow_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+#ifdef POW_TEST_HOOKS
   pow_aql_close(ctx->aql);
+#endif
   (void)hipFree(ctx->d_blob);
   if (ctx->h_blob) (void)hipHostFree(ctx->h_blob);
   (void)hipFree(ctx->d_tail);
@@ -662,16 +765,21 @@ int pow_warmup(pow_ctx* ctx) {
   memset(&M, 0, sizeof M);
   HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, 0));  // publishes done = 0: never a live seq
   HIP_OK(hipStreamSynchronize(ctx->stream));
+#ifdef POW_TEST_HOOKS
   if (ctx->aql) {  // the same launches once through the direct-dispatch queue (its first packets)
     for (int k = 0; k < 9; ++k) {
-      if (int rc = k < 8 ? launch_search_lat(ctx, k & 1, k & 2, k & 4, 1, LL) : launch_hash_one(ctx, M, 0)) return rc;
+      const uint64_t deadline = mono_ns() + ctx->watchdog_ns;
+      if (int rc = k < 8 ? launch_search_lat(ctx, k & 1, k & 2, k & 4, 1, LL, deadline)
+                         : launch_hash_one(ctx, M, 0, deadline))
+        return rc;
       for (int st, n = 0; (st = pow_aql_status(ctx->aql)) != 0; ++n) {
         if (st < 0) return fail(POW_EHIP, "warm-up dispatch: queue error 0x%x", -st);
-        if (n > 20000) break;  // POW_AQL_EXP_NO_SIGNAL (test library): no completion to wait for; ~20 ms
+        if (n > 20000) break;  // POW_AQL_EXP_NO_SIGNAL: no completion to wait for; ~20 ms
         std::this_thread::sleep_for(std::chrono::microseconds(1));
       }
     }
   }
+#endif
   pow_block b;
   memset(&b, 0, sizeof b);
   return pow_hash_blocks(ctx, &b, 1, nullptr, nullptr);
@@ -679,7 +787,10 @@ int pow_warmup(pow_ctx* ctx) {
 
 int pow_launch_path(const pow_ctx* ctx) {
   if (!ctx) return fail(POW_EINVAL, "null");
-  return ctx->aql ? POW_LAUNCH_DIRECT : POW_LAUNCH_HIP;
+#ifdef POW_TEST_HOOKS
+  if (ctx->aql) return POW_LAUNCH_DIRECT;
+#endif
+  return POW_LAUNCH_HIP;
 }
 
 int pow_get_stats(const pow_ctx* ctx, pow_stats* out) {
@@ -750,8 +861,9 @@ int hash_one(pow_ctx* ctx, const pow_block* b, uint8_t* digest, char* hex) {
   }
   if (++ctx->one_seq == 0) ctx->one_seq = 1;  // never 0: the warm-up launch publishes 0
   const uint32_t seq = ctx->one_seq;
-  if (int rc = launch_hash_one(ctx, M, seq)) return rc;
-  if (int rc = wait_published(ctx, &ctx->h_one->done, seq, "hash kernel")) return rc;
+  const uint64_t t0 = mono_ns(), deadline = t0 + ctx->watchdog_ns;
+  if (int rc = launch_hash_one(ctx, M, seq, deadline)) return rc;
+  if (int rc = wait_published(ctx, &ctx->h_one->done, seq, "hash kernel", t0, deadline)) return rc;
   uint32_t dg[8];
   for (int k = 0; k < 8; ++k) dg[k] = __atomic_load_n(&ctx->h_one->digest[k], __ATOMIC_RELAXED);
   ctx->stats = pow_stats{(double)ctx->h_one->ticks / ctx->realtime_khz, 1u, 1u};

@@ -2,11 +2,12 @@
 // K1' pow_search_lat): an AQL kernel-dispatch packet written into an HSA queue
 // of the library's own and its doorbell rung, instead of hipLaunchKernel.
 //
-// Why: these launches are latency-bound.  A block validation (pow_hash_block,
-// valid_new_block / validate_block_for_chain, node.cpp:199-253) is ~10 us of
-// kernel on one wave, and the HIP launch path adds ~8-10 us around it, with a
-// wide spread from process to process (DESIGN.md §4 K2').  Writing the packet
-// takes ~2 us, most of it the PCIe read-back below.
+// TEST LIBRARY ONLY since round 5 (libpow_gpu_test.so, opt-in with POW_AQL=1).
+// It saved 1-2 us per launch at d <= 13 and nothing above (DESIGN.md §4 K2'),
+// and the one unexplained protocol failure of round 4 happened under it, so
+// the shipped libpow_gpu.so launches every kernel through hipLaunchKernel.  It
+// stays here for the dispatch A/B (tools/abttb_sweep.sh) and for the
+// multi-producer ordering test (POW_AQL_EXP_STALL_HEADER below).
 //
 // What is dispatched is the library's own code: the gfx950 code object is
 // copied out of the offload bundle embedded in this shared library's file (the
@@ -18,21 +19,27 @@
 //
 // Memory protocol of a dispatch:
 //  * arguments: a ring of device memory, uncached on the GPU side, written by
-//    the host through the BAR; then an HDP flush and a read-back of the last
-//    word, so they are in HBM before the doorbell;
+//    the host through the BAR (pow_aql_open checks the host can reach it);
+//    then an HDP flush and a read-back of the last word, so they are in HBM
+//    before the doorbell;
 //  * acquire fence at AGENT scope: no L2 invalidate at the start of every
 //    launch (at system scope K1' at d = 9 ran 17 us instead of 15: its code
-//    and tables came from HBM again).  Nothing the kernels read needs it: the
-//    arguments are uncached, the result words (PowResult) are written by the
-//    previous launch on this device, and host-memory words (cancel epoch, stop
-//    board) are read with system-scope atomics in the kernels;
+//    and tables came from HBM again);
 //  * release fence at system scope, and a completion signal per context that
 //    counts its launches in flight, so a launch that ends without publishing
 //    its result is still seen;
-//  * one queue per device and process (pow_aql_open), packets without the
-//    barrier bit: each context orders its own launches by waiting for each
-//    one's result, and one context's validation does not wait behind
-//    another's running search.
+//  * one queue per device and process (pow_aql_open), HSA_QUEUE_TYPE_MULTI,
+//    packets without the barrier bit: each context orders its own launches by
+//    waiting for each one's result.
+// Multi-producer ordering ("the ordering argument"): a producer
+// reserves its index (atomic add on the write index), waits for the slot to be
+// free (read index > idx - size), writes the body, stores the 32-bit
+// header+setup word with release semantics, then rings the doorbell with idx.
+// It relies on three statements of hsa.h (ROCm 7.2): every slot starts
+// INVALID and a processed slot is INVALID again ("processed in the past, but
+// not reassigned", hsa.h:2816-2820); a packet processor must not process an
+// INVALID packet (same lines); and on a MULTI queue the doorbell "can be
+// updated with any value" (hsa.h:2343-2346), i.e. out of order.
 // Any failure to set this up leaves the caller on the HIP launch path (the
 // same kernels).
 #include <dlfcn.h>
@@ -41,10 +48,12 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -123,10 +132,15 @@ void release_all() {
   }
 }
 
+// The HSA agent of HIP device `device` (the current device): the owner of a
+// probe allocation made on it.  Matching on PCI bus/device/domain is not
+// enough: in a partition mode (CPX, DPX) several agents share them and differ
+// only in the function bits.  Without the pointer query, a BDF match is used
+// only when it is unique.
 struct AgentSearch {
-  uint32_t bus, dev, domain;
+  uint32_t bdf, domain;
   hsa_agent_t found{};
-  bool ok = false;
+  int matches = 0;
 };
 
 hsa_status_t match_agent(hsa_agent_t a, void* p) {
@@ -137,11 +151,32 @@ hsa_status_t match_agent(hsa_agent_t a, void* p) {
   uint32_t bdf = 0, dom = 0;
   hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
   hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
-  if (!s->ok && ((bdf >> 8) & 0xFF) == s->bus && ((bdf >> 3) & 0x1F) == s->dev && dom == s->domain) {
-    s->found = a;
-    s->ok = true;
+  if ((bdf & 0xFFF8u) == (s->bdf & 0xFFF8u) && dom == s->domain) {
+    if (s->matches++ == 0) s->found = a;
   }
   return HSA_STATUS_SUCCESS;
+}
+
+bool device_agent(int device, const hipDeviceProp_t& prop, hsa_agent_t* out, std::string& why) {
+  void* probe = nullptr;
+  if (hipSetDevice(device) == hipSuccess && hipMalloc(&probe, 64) == hipSuccess) {
+    hsa_amd_pointer_info_t info{};
+    info.size = sizeof info;
+    const bool ok = hsa_amd_pointer_info(probe, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+                    info.type == HSA_EXT_POINTER_TYPE_HSA && info.agentOwner.handle != 0;
+    (void)hipFree(probe);
+    if (ok) {
+      *out = info.agentOwner;
+      return true;
+    }
+  }
+  AgentSearch s{((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3), (uint32_t)prop.pciDomainID};
+  if (hsa_iterate_agents(match_agent, &s) != HSA_STATUS_SUCCESS || s.matches != 1) {
+    why = s.matches > 1 ? "several HSA agents share the device's PCI address (partition mode)" : "no HSA agent for the device";
+    return false;
+  }
+  *out = s.found;
+  return true;
 }
 
 // The gfx950 code object holding the kernels, out of the offload bundles that
@@ -215,9 +250,7 @@ DeviceKernels* device_kernels(int device) {
   if (hsa_init() != HSA_STATUS_SUCCESS) return bail("hsa_init");  // reference-counted; the HIP runtime holds one
   D.hsa_up = true;
   if (!g_atexit) g_atexit = atexit(release_all) == 0;
-  AgentSearch s{(uint32_t)prop.pciBusID, (uint32_t)prop.pciDeviceID, (uint32_t)prop.pciDomainID};
-  if (hsa_iterate_agents(match_agent, &s) != HSA_STATUS_SUCCESS || !s.ok) return bail("no HSA agent for the device");
-  D.agent = s.found;
+  if (!device_agent(device, prop, &D.agent, D.why)) return bail(D.why);
   if (!own_code_object(D.code, D.why)) return bail(D.why);
   if (hsa_code_object_reader_create_from_memory(D.code.data(), D.code.size(), &D.reader) != HSA_STATUS_SUCCESS)
     return bail("hsa_code_object_reader_create_from_memory");
@@ -270,11 +303,19 @@ struct pow_aql {
   uint8_t* ring = nullptr;   // kernel-argument slots: device memory the host writes
   int ring_kind = 0;         // 1 host memory, 2 device memory
   uint32_t next_slot = 0;    // this context's launches so far (ring slot = next_slot % kQueueSize)
+  uint64_t last_idx = ~0ull; // packet index of this context's last dispatch (the watchdog's diagnostic)
+  unsigned stall_us = 0;     // POW_AQL_EXP_STALL_HEADER: sleep between body and header
 };
 
 namespace {
 void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
   static_cast<std::atomic<int>*>(data)->store((int)st, std::memory_order_release);
+}
+
+uint64_t now_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
 }
 }  // namespace
 
@@ -309,11 +350,21 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
     if (why) *why = "hsa_queue_create";
     return -1;
   }
+  // A queue that has reported an error is dead for the rest of the process:
+  // new contexts stay on the HIP launch path.
+  if (!(flags & POW_AQL_EXP_OWN_QUEUE) && dk->queue_error.load(std::memory_order_acquire)) {
+    if (why) *why = "the device's dispatch queue reported an error earlier in this process";
+    return -1;
+  }
   pow_aql* a = new pow_aql;
   a->dk = dk;
   a->flags = flags;
   a->q = shared;
   a->queue_error = &dk->queue_error;
+  if (flags & POW_AQL_EXP_STALL_HEADER) {
+    const char* e = getenv("POW_AQL_STALL_US");
+    a->stall_us = e ? (unsigned)strtoul(e, nullptr, 0) : 200000u;
+  }
   auto bail = [&](const char* w) {
     if (why) *why = w;
     pow_aql_close(a);
@@ -333,6 +384,13 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
                               (flags & POW_AQL_EXP_FINE_ARGS) ? hipDeviceMallocFinegrained
                                                               : hipDeviceMallocUncached) != hipSuccess)
       return bail("kernel-argument ring");
+    // The host writes the ring with plain stores: it must be mapped into the
+    // host's address space (large BAR).  Otherwise the first dispatch would
+    // fault instead of taking the HIP launch path.
+    hsa_amd_pointer_info_t info{};
+    info.size = sizeof info;
+    if (hsa_amd_pointer_info(a->ring, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS || !info.hostBaseAddress)
+      return bail("the kernel-argument ring is not host-accessible (no large BAR)");
   }
   // A signal only the GPU's packet processor writes and the host reads: no
   // interrupt event behind it (the host never sleeps on it).
@@ -356,8 +414,8 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
 void pow_aql_close(pow_aql* a) {
   if (!a) return;
   // Launches are host-waited, so none of this context's is in flight unless
-  // one failed mid-flight: wait (bounded) for the last one to complete before
-  // its argument ring and signal go.
+  // one failed mid-flight: wait (bounded, ~1 s) for the last one to complete
+  // before its argument ring and signal go.
   for (int n = 0; n < 1000000 && a->signal_up && a->q && hsa_signal_load_scacquire(a->done) != 0 &&
                   !a->queue_error->load(std::memory_order_acquire);
        ++n)
@@ -375,13 +433,36 @@ int pow_aql_status(const pow_aql* a) {
   return hsa_signal_load_scacquire(a->done) == 0 ? 0 : 1;
 }
 
+std::string pow_aql_diag(const pow_aql* a) {
+  char buf[320];
+  const hsa_queue_t* q = a->q;
+  const uint64_t rd = hsa_queue_load_read_index_scacquire(q), wr = hsa_queue_load_write_index_scacquire(q);
+  uint32_t word = 0;
+  if (a->last_idx != ~0ull)
+    word = __atomic_load_n((const uint32_t*)((const hsa_kernel_dispatch_packet_t*)q->base_address + (a->last_idx % q->size)),
+                           __ATOMIC_ACQUIRE);
+  const long long sig = a->signal_up ? (long long)hsa_signal_load_scacquire(a->done) : -1;
+  snprintf(buf, sizeof buf,
+           "completion signal %lld (launches in flight), queue read index %llu, write index %llu, "
+           "this context's last packet index %lld, header at its slot 0x%04x (type %u; 1 = INVALID), queue error 0x%x",
+           sig, (unsigned long long)rd, (unsigned long long)wr, a->last_idx == ~0ull ? -1ll : (long long)a->last_idx,
+           word & 0xFFFFu, (word >> HSA_PACKET_HEADER_TYPE) & ((1u << HSA_PACKET_HEADER_WIDTH_TYPE) - 1u),
+           (unsigned)a->queue_error->load(std::memory_order_acquire));
+  return buf;
+}
+
 int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_size, const void* args,
-                     uint32_t nbytes) {
+                     uint32_t nbytes, uint64_t deadline_ns, std::string* why) {
+  auto refuse = [&](const char* w) {
+    if (why) *why = w;
+    return -1;
+  };
   if (kernel < 0 || kernel >= POW_AQL_NKERNELS || !args || workgroups == 0 || wg_size == 0 || wg_size > 1024 ||
       (uint64_t)workgroups * wg_size > 0xFFFFFFFFull)
-    return -1;
+    return refuse("bad launch geometry");
   const DeviceKernels::Kern& K = a->dk->k[kernel];
-  if (nbytes != K.kernarg || a->queue_error->load(std::memory_order_acquire)) return -1;
+  if (nbytes != K.kernarg) return refuse("argument size");
+  if (a->queue_error->load(std::memory_order_acquire)) return refuse("the queue reported an error");
   hsa_queue_t* q = a->q;
   // This context's argument slot: its launches are host-waited, so the slot's
   // previous user (kQueueSize launches ago) has finished reading it.
@@ -401,16 +482,23 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
     __atomic_store_n((volatile uint32_t*)a->dk->hdp_flush, 1u, __ATOMIC_RELAXED);
     if (!(a->flags & POW_AQL_EXP_NO_READBACK)) (void)*(volatile uint32_t*)(arg + nbytes - 4);
   }
+  // The packet slot is free once the packet processor has read past
+  // idx - size (at most a few packets are ever outstanding).  A slot that
+  // stays busy past the deadline means the packet processor has stopped
+  // consuming this queue: the reserved slot is left INVALID (nothing may be
+  // written into a slot the processor has not released), and the caller gets
+  // the error and the diagnostic.
+  const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
+  a->last_idx = idx;
+  for (uint32_t n = 0; idx - hsa_queue_load_read_index_scacquire(q) >= q->size; ++n) {
+    if (a->queue_error->load(std::memory_order_acquire)) return refuse("the queue reported an error");
+    if ((n & 1023u) == 1023u && now_ns() > deadline_ns) return refuse("no free packet slot before the deadline");
+  }
   // in flight += 1; the packet processor subtracts 1 when the launch
   // completes (which may be after the caller has seen the kernel's done word
   // and started the next launch: a count, not a flag)
   const bool sig = !(a->flags & POW_AQL_EXP_NO_SIGNAL);
   if (sig) hsa_signal_add_scacq_screl(a->done, 1);
-  // The packet slot is free once the packet processor has read past
-  // idx - size (at most a few packets are ever outstanding).
-  const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
-  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size)
-    if (a->queue_error->load(std::memory_order_acquire)) return -1;
   hsa_kernel_dispatch_packet_t* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx % q->size);
   memset((uint8_t*)pk + 4, 0, sizeof *pk - 4);  // everything but header + setup, which go last
   pk->workgroup_size_x = (uint16_t)wg_size;
@@ -431,6 +519,9 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
                                      (((a->flags & POW_AQL_EXP_RELEASE_AGENT) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM)
                                       << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  // The ordering test's hook: a producer descheduled between its reservation
+  // and its header store, while other producers' later packets go in.
+  if (a->stall_us) usleep(a->stall_us);
   __atomic_store_n((uint32_t*)pk, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
   return 0;

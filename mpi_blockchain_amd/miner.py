@@ -81,8 +81,10 @@ class GpuMiner:
         return {"cu_count": cu.value, "clock_khz": clk.value, "name": name.value.decode()}
 
     def launch_path(self) -> str:
-        """"direct" (AQL packets into the context's own queue) or "hip"
-        (hipLaunchKernel) for the latency-bound launches (pow_launch_path)."""
+        """How the latency-bound launches go out (pow_launch_path): "hip"
+        (hipLaunchKernel; the shipped library's only path) or "direct" (AQL
+        packets into the process's dispatch queue: test library with
+        POW_AQL=1)."""
         return "direct" if check(self.L.pow_launch_path(self.ctx), self.L) == 1 else "hip"
 
     def stats(self) -> dict:

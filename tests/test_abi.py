@@ -39,7 +39,7 @@ def test_library_exports_all_symbols():
 
 
 HOOKS = (b"POW_FAULT_INJECT", b"POW_FORCE_FULL", b"POW_LAT_MAX", b"POW_LAT_WPS", b"POW_GRID_PER_CU", b"POW_TEST_SENTINEL_IDLE",
-         b"POW_TEST_RCCL_LIB", b"POW_NO_AQL", b"POW_AQL_EXP")
+         b"POW_TEST_RCCL_LIB", b"POW_AQL", b"POW_AQL_EXP", b"POW_AQL_STALL_US", b"POW_WATCHDOG_MS", b"POW_TEST_STALL_US")
 
 
 def test_shipped_library_has_no_test_hooks():
@@ -55,6 +55,21 @@ def test_shipped_library_has_no_test_hooks():
     assert T is not _lib.load()
     for name in header_functions():
         assert hasattr(T, name), name
+
+
+def test_shipped_library_launches_through_hip_only():
+    """Round 5: direct AQL dispatch (pow_aql.cpp) is linked into the test
+    library only.  The shipped library neither links the HSA runtime nor holds
+    the dispatcher or the offload-bundle reader: every kernel goes out through
+    hipLaunchKernel."""
+    shipped = open(_lib.LIB_PATH, "rb").read()
+    test = open(_lib.TEST_LIB_PATH, "rb").read()
+    for marker in (b"libhsa-runtime64", b"pow_aql_open"):
+        assert marker not in shipped, marker
+    assert b"libhsa-runtime64" in test and b"pow_aql_open" in test
+    # the watchdog's diagnostics are in both
+    for lib in (shipped, test):
+        assert b"watchdog: no result after" in lib and b"watchdog: not complete after" in lib
 
 
 def test_block_layout():

@@ -118,26 +118,26 @@ def test_single_block_path(miner, golden, templates):
 
 def test_launch_paths(miner, golden, templates):
     """The latency-bound launches (K2' here, K1' in pow_mine's first sub-round)
-    go out as AQL packets on the context's own queue (pow_aql.cpp) in the
-    shipped library; the test library's POW_NO_AQL=1 keeps them on
-    hipLaunchKernel, the fallback.  Both give the reference's digests and the
+    go through hipLaunchKernel in the shipped library (round 5).  The test
+    library's POW_AQL=1 sends them as AQL packets into the process's dispatch
+    queue (pow_aql.cpp) instead.  Both give the reference's digests and the
     same lowest solution."""
-    assert miner.launch_path() == "direct"
-    hip = hooked_miner(POW_NO_AQL=1)
+    assert miner.launch_path() == "hip"
+    direct = hooked_miner(POW_AQL=1)
     try:
-        assert hip.launch_path() == "hip"
+        assert direct.launch_path() == "direct"
         for e in golden["random_blocks"]:
             b = block_from_random(e)
-            assert hip.block_to_hash(b) == miner.block_to_hash(b) == e["hex"]
+            assert direct.block_to_hash(b) == miner.block_to_hash(b) == e["hex"]
         w = golden["windows"][0]
         b = block_from_template(templates[w["template"]])
         for d, st in w["sets"].items():
             if st["count"]:
                 want = w["start"] + st["counters"][0]
                 assert miner.mine(b, w["start"], w["count"], int(d)).counter == want
-                assert hip.mine(b, w["start"], w["count"], int(d)).counter == want
+                assert direct.mine(b, w["start"], w["count"], int(d)).counter == want
     finally:
-        hip.close()
+        direct.close()
 
 
 def test_messages(golden, templates):
@@ -339,9 +339,10 @@ def test_validation_beside_mining():
 def test_direct_dispatch_two_threads(golden, templates):
     """Two contexts of one process driven from two threads at once, as in a
     pow_node rank (miner thread: pow_mine_any on K1', receive thread:
-    pow_hash_block on K2'): both put packets into the process's one dispatch
-    queue (pow_aql.cpp, no barrier bit).  Every result must stay exact: the
-    lowest solutions of the golden window and the reference's digests."""
+    pow_hash_block on K2'), both on direct dispatch (test library, POW_AQL=1):
+    both put packets into the process's one dispatch queue (pow_aql.cpp, no
+    barrier bit).  Every result must stay exact: the lowest solutions of the
+    golden window and the reference's digests."""
     import threading
 
     w = golden["windows"][0]
@@ -350,7 +351,7 @@ def test_direct_dispatch_two_threads(golden, templates):
     blocks = [block_from_random(e) for e in golden["random_blocks"]]
     want = [e["hex"] for e in golden["random_blocks"]]
     errors = []
-    with GpuMiner(0) as m, GpuMiner(0) as v:
+    with hooked_miner(POW_AQL=1) as m, hooked_miner(POW_AQL=1) as v:
         assert m.launch_path() == v.launch_path() == "direct"
 
         def mine_loop():
@@ -377,6 +378,128 @@ def test_direct_dispatch_two_threads(golden, templates):
         assert not th.is_alive()
     assert not errors, errors[:5]
     assert n >= len(blocks)
+
+
+def _timed_hash(m, b, out, key):
+    import time
+
+    t = time.perf_counter()
+    try:
+        out[key] = (m.block_to_hash(b), time.perf_counter() - t)
+    except Exception as e:  # reported by the caller
+        out[key] = (e, time.perf_counter() - t)
+
+
+def test_direct_dispatch_stalled_producer(golden):
+    """The multi-producer ordering argument (pow_aql.cpp header),
+    forced instead of left to timing.  Producer A (POW_AQL_EXP_STALL_HEADER)
+    reserves packet index i, writes the body and then sleeps 200 ms before it
+    stores the header and rings the doorbell with i.  Meanwhile producer B, on
+    the same queue, takes i + 1, stores its header and rings the doorbell with
+    i + 1 (a larger doorbell value first, then a smaller one).  Both launches
+    must give the reference's digests; B's packet must not run before A's
+    header is in (the packet processor does not process an INVALID slot, and
+    takes packets in order), so B returns only after A's stall."""
+    import threading
+    import time
+
+    blocks = [block_from_random(e) for e in golden["random_blocks"][:2]]
+    want = [e["hex"] for e in golden["random_blocks"][:2]]
+    a = hooked_miner(POW_AQL=1, POW_AQL_EXP=512, POW_AQL_STALL_US=200000)
+    b = hooked_miner(POW_AQL=1)
+    try:
+        assert a.launch_path() == b.launch_path() == "direct"
+        out = {}
+        for rep in range(3):
+            th = threading.Thread(target=_timed_hash, args=(a, blocks[0], out, "a"))
+            th.start()
+            time.sleep(0.05)  # A is inside its stall: index reserved, header not stored
+            _timed_hash(b, blocks[1], out, "b")
+            th.join(timeout=30)
+            assert not th.is_alive()
+            assert out["a"][0] == want[0] and out["b"][0] == want[1], out
+            print(f"stalled producer, rep {rep}: A {out['a'][1] * 1e3:.1f} ms, B (behind A) {out['b'][1] * 1e3:.1f} ms")
+            assert out["b"][1] > 0.1, out  # held behind A's INVALID slot until A's header went in
+            # and unstalled, B alone is fast again
+            t = time.perf_counter()
+            assert b.block_to_hash(blocks[1]) == want[1]
+            assert time.perf_counter() - t < 0.05
+    finally:
+        a.close()
+        b.close()
+
+
+def test_watchdog_direct_dispatch(golden):
+    """A launch held in the queue past the watchdog's deadline is reported,
+    not waited for: producer C (POW_WATCHDOG_MS=50) dispatches behind A's
+    stalled slot (POW_AQL_EXP_STALL_HEADER, 400 ms).  C's call fails with
+    POW_EHIP and the diagnostic (seq, done word, completion signal, the
+    queue's read/write index, C's packet index and the header in its slot);
+    the queue's read index has not reached C's packet.  A's launch and, once
+    A's header is in, C's packet still complete: nothing is left wedged."""
+    import re
+    import threading
+    import time
+
+    from mpi_blockchain_amd._lib import PowError
+
+    blocks = [block_from_random(e) for e in golden["random_blocks"][:2]]
+    want = [e["hex"] for e in golden["random_blocks"][:2]]
+    a = hooked_miner(POW_AQL=1, POW_AQL_EXP=512, POW_AQL_STALL_US=400000)
+    c = hooked_miner(POW_AQL=1, POW_WATCHDOG_MS=50)
+    try:
+        out = {}
+        th = threading.Thread(target=_timed_hash, args=(a, blocks[0], out, "a"))
+        th.start()
+        time.sleep(0.05)
+        with pytest.raises(PowError) as ei:
+            c.block_to_hash(blocks[1])
+        msg = str(ei.value)
+        print(msg)
+        assert "hash kernel: watchdog: no result after" in msg and "launch path direct" in msg, msg
+        m = re.search(r"read index (\d+), write index (\d+), this context's last packet index (\d+), "
+                      r"header at its slot 0x([0-9a-f]+) \(type (\d+)", msg)
+        assert m, msg
+        rd, wr, idx, typ = int(m.group(1)), int(m.group(2)), int(m.group(3)), int(m.group(5))
+        assert rd <= idx < wr and typ == 2, msg  # C's packet is valid and waits behind A's slot
+        th.join(timeout=30)
+        assert not th.is_alive() and out["a"][0] == want[0], out
+    finally:
+        a.close()
+        c.close()  # waits (bounded) for C's packet, which runs once A's header is in
+
+
+@pytest.mark.parametrize("what", ["hash_one", "latency", "search"])
+def test_watchdog_hip_path(golden, templates, what):
+    """The same watchdog on the HIP launch path (the shipped one): the test
+    library's POW_TEST_STALL_US puts a bounded 300 ms stall kernel in front
+    of each launch on the context's stream, and POW_WATCHDOG_MS=30 makes the
+    host's wait give up first.  K2' (pow_hash_block), K1' (first sub-round of
+    pow_mine) and K1 (pow_sweep) each fail with POW_EHIP and a watchdog
+    diagnostic instead of waiting."""
+    from mpi_blockchain_amd._lib import PowError
+
+    m = hooked_miner(POW_TEST_STALL_US=300000, POW_WATCHDOG_MS=30)
+    try:
+        assert m.launch_path() == "hip"
+        b = block_from_random(golden["random_blocks"][0])
+        tmpl = block_from_template(templates["S0"])
+        with pytest.raises(PowError) as ei:
+            if what == "hash_one":
+                m.block_to_hash(b)
+            elif what == "latency":
+                m.mine(tmpl, 0, 1 << 20, 9)
+            else:
+                m.sweep(tmpl, 0, 1 << 20, 9)
+        msg = str(ei.value)
+        print(msg)
+        key = {"hash_one": "hash kernel: watchdog: no result after",
+               "latency": "latency kernel: watchdog: no result after",
+               "search": "watchdog: not complete after"}[what]
+        assert key in msg, msg
+        assert "launch path hip" in msg or what == "search", msg
+    finally:
+        m.close()  # synchronises the stream: the stall kernel ends on its own
 
 
 def test_chained_blocks_validate(miner):
@@ -548,15 +671,15 @@ def test_parity_fuzz():
     assert res["cases"] == 120 and res["solutions"] > 0
 
 
-@pytest.mark.parametrize("env", [{"POW_LAT_WPS": 4}, {"POW_LAT_WPS": 4, "POW_FORCE_FULL": 1}, {"POW_NO_AQL": 1}],
-                         ids=["lat_asm", "lat_asm_full", "hip_launch"])
+@pytest.mark.parametrize("env", [{"POW_LAT_WPS": 4}, {"POW_LAT_WPS": 4, "POW_FORCE_FULL": 1}, {"POW_AQL": 1}],
+                         ids=["lat_asm", "lat_asm_full", "direct_dispatch"])
 def test_parity_fuzz_latency_asm_variants(env):
     """The latency kernel's asm-group variants (pow_search_lat<*, *, true>, run
     by the plan only at d = 20-21, 4 waves per SIMD) under the same exact
     oracle comparison: the test library forces 4 waves per SIMD at every d,
     and with POW_FORCE_FULL the d > 32 variants <true, *, true> as well.
-    hip_launch: the plan's kernels launched through hipLaunchKernel (the
-    fallback when the direct dispatch queue cannot be set up)."""
+    direct_dispatch: the plan's kernels sent as AQL packets (test library,
+    POW_AQL=1) instead of the shipped hipLaunchKernel."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import parity_fuzz
 

@@ -25,6 +25,17 @@ REF_BIN = os.path.join(ROOT, "oracle", "_ref", "blockchain_ref")
 
 
 FORK_MSGS = ("Perdí la carrera", "Conflicto suave", "TAG_CHAIN_HASH")
+
+
+def keep_log(run, name, wall=None):
+    """Diagnostics: with POW_NODE_LOG_DIR set (tools/gpu_pass.sh sets it under
+    gpurun_out/), every network's whole output is kept, so a failing pass's
+    log survives the re-runs that follow it."""
+    d = os.environ.get("POW_NODE_LOG_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{name}.log"), "w") as f:
+            f.write(f"rc {run.returncode}" + (f" wall {wall:.3f} s" if wall is not None else "") + f"\n{run.stdout}")
 # A rival block 1 received while this rank's chain is at index 1 (node.cpp:235)
 # or already past it (node.cpp:242): the fork --hold-first forces.
 RIVAL_BLOCK1 = re.compile(r"Conflicto suave: (Conflicto de branch \(1\)|Descarto el bloque \(1 vs \d+\))")
@@ -42,9 +53,7 @@ def test_gpu_network(tmp_path, np_, d):
     extra = ("--hold-first", "1", "--winner-pause-us", "3000") if d <= 5 else ()
     t0 = time.perf_counter()
     run = run_network(np_, str(tmp_path), difficulty=d, blocks=10, timeout=240, extra_args=extra)
-    if os.environ.get("POW_NODE_LOG_DIR"):  # diagnostics: keep the network's output
-        with open(os.path.join(os.environ["POW_NODE_LOG_DIR"], f"net_{np_}_{d}.log"), "w") as f:
-            f.write(f"wall {time.perf_counter() - t0:.3f} s rc {run.returncode}\n{run.stdout}")
+    keep_log(run, f"net_{np_}_{d}", time.perf_counter() - t0)
     assert run.returncode == 0, run.stdout[-3000:]
     assert "Error duro" not in run.stdout
     complete = [r for r, entries in run.chains.items() if check_chain(entries, 10, d)]
@@ -99,6 +108,7 @@ def test_mixed_with_reference_nodes(tmp_path):
     # profiles/r02/verify/protocol_soak_mixed_*.log).
     run = run_network(2, str(tmp_path), difficulty=9, blocks=10, timeout=240, ref_binary=REF_BIN, n_ref=2,
                       extra_args=("--serial-init", "1", "--idle-below", "3"))
+    keep_log(run, "mixed_2ref_2gpu")
     out = run.stdout
     assert run.returncode == 0, out[-3000:]
     assert "Error duro" not in out, out[-3000:]
@@ -130,8 +140,12 @@ def test_mutual_chain_request(tmp_path, np_):
     la carrera por varios"), asks the tip's owner for its chain while that
     owner asks it, serves the owner's TAG_CHAIN_HASH inside its own wait,
     receives the chain, checks it and splices it in (find = 2: block 1 is the
-    common point with genesis).  The network then finishes its 10 blocks."""
+    common point with genesis).  No rank mines block 4 before every rank has
+    migrated (pow_node_test's second barrier, round 5), so the first rank to
+    finish cannot abort the job before a slower rank has logged its migration.
+    The network then finishes its 10 blocks."""
     run = run_network(np_, str(tmp_path), difficulty=9, blocks=10, timeout=120, extra_args=("--private-lead", "3"))
+    keep_log(run, f"mutual_{np_}")
     out = run.stdout
     assert run.returncode == 0, out[-3000:]
     assert "Error duro" not in out, out[-3000:]

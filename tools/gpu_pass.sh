@@ -7,7 +7,7 @@
 #   tests            the whole GPU suite (pytest -m gpu)
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (default: N = 1, every block of the JSON line)
-#   profile          tools/profile_round.sh r04 (kernel trace + 4 PMC passes of the bench workload)
+#   profile          tools/profile_round.sh r05 (kernel trace + 4 PMC passes of the bench workload)
 #   fuzz             randomised parity, shipped library: 1,000 cases (tests/parity_fuzz.py)
 #   fuzz_big         10,000 cases, then 2,000 each on the test library: K1' asm variants
 #                    (POW_LAT_WPS=4), + d > 32 variants, and K1 alone (POW_LAT_MAX=0)
@@ -31,10 +31,11 @@ cd "$R"
 while [ $# -gt 0 ]; do
   step=$1; shift
   case "$step" in
-    tests) $S gputests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread || exit $? ;;
+    tests) POW_NODE_LOG_DIR="$R/gpurun_out/netlogs" \
+             $S gputests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread || exit $? ;;
     smoke) $S smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) $S bench 900 python -u bench.py || exit $? ;;
-    profile) bash "$R/tools/profile_round.sh" r04 || exit $? ;;
+    profile) bash "$R/tools/profile_round.sh" r05 || exit $? ;;
     fuzz) $S fuzz 900 python -u tests/parity_fuzz.py --cases 1000 --seed 404 || exit $? ;;
     fuzz_big) $S fuzz_big 900 python -u tests/parity_fuzz.py --cases 10000 --seed 4004 &&
       POW_LAT_WPS=4 $S fuzz_lat_asm 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4005 &&
