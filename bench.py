@@ -477,30 +477,95 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
     over every GPU of the job (collective; the same templates on every rank).
     Each rank mines its static shard; the first hit stops the node's other
     GPUs inside their launches (stop board) and one all-reduce agrees on the
-    winner.  Expected trials per block 2^d; strong scaling in N."""
+    winner.  Expected trials per block 2^d; strong scaling in N.
+
+    Every winner is verified (outside the timed calls): its nonce is the
+    counter's, its digest recomputed by pow_hash_block is the block_hash it
+    carries and solves d (solves_problem, block.cpp:91-96), the counter lies in
+    the searched range, and every rank reports the same counter (all-reduce
+    min == max).  The verdicts are all-reduced too, so every rank sees the
+    same `verified` block."""
     import random
 
-    from mpi_blockchain_amd.block import make_block
+    from mpi_blockchain_amd.block import field, make_block, nonce_from_counter, solves_problem
+    from mpi_blockchain_amd.miner import block_hex
 
+    U64MAX = (1 << 64) - 1
+    span = 1 << 48
     rng = random.Random(1)
     times, hashes, counters = [], [], []
+    bad = {"no_winner": 0, "nonce": 0, "digest": 0, "solves": 0, "range": 0, "ranks_disagree": 0}
     for _ in range(n_templates):
         b = make_block(rng.randrange(1, 1 << 16), 0, 9, 1700000000 + rng.randrange(256),
                        bytes(rng.randrange(256) for _ in range(32)).hex().encode())
         group.allreduce([0], "sum")  # line the ranks up
         t = time.perf_counter()
-        r = group.mine(b, 0, 1 << 48, d, any_solution=True)
+        r = group.mine(b, 0, span, d, any_solution=True)
         times.append(time.perf_counter() - t)
         hashes.append(group.allreduce([r.hashes if r else 0], "sum")[0])
+        c = r.counter if r else U64MAX
         counters.append(r.counter if r else None)
+        lo, hi = group.allreduce([c], "min")[0], group.allreduce([c], "max")[0]
+        v = [0] * 6
+        if r is None:
+            v[0] = 1
+        else:
+            hx = block_hex(r.block)
+            v[1] = int(field(r.block, "nonce") != nonce_from_counter(c))
+            v[2] = int(group.miner.block_to_hash(r.block) != hx)
+            v[3] = int(not solves_problem(hx, d))
+            v[4] = int(not 0 <= c < span)
+        v[5] = int(lo != hi)
+        for k, x in zip(bad, group.allreduce(v, "max")):
+            bad[k] += x
     tot_t = sum(times)
+    verified = {"winners_checked": n_templates, "failures": bad, "ok": not any(bad.values()),
+                "how": "nonce == counter's, pow_hash_block(winner) == its block_hash, solves_problem(hash, d), "
+                       "0 <= counter < 2^48, all-reduce(min) == all-reduce(max) of the ranks' counters"}
     return {"difficulty_bits": d, "templates": n_templates, "n_gpus": world,
             "time_to_block_ms_median": round(1e3 * statistics.median(times), 3),
             "time_to_block_ms_mean": round(1e3 * tot_t / n_templates, 3),
             "expected_hashes": 2 ** d, "hashes_all_ranks_mean": int(sum(hashes) / n_templates),
             "hashes_per_s_all_ranks": round(sum(hashes) / tot_t, 1),
+            "counters": counters, "verified": verified,
             "note": "pow_group_mine_any over all GPUs (static shards, stop board, one all-reduce per round); "
                     "hashes include the trials peers ran before the winner's hit reached them"}
+
+
+def rank_topology(rank: int, local: int, group) -> dict:
+    """What this rank ran on: its HIP device and the device's PCI address and
+    UUID (torch.cuda.get_device_properties), and RCCL's own view of the
+    group's communicator (pow_group_info: ncclCommCount, ncclCommCuDevice)."""
+    import torch
+
+    p = torch.cuda.get_device_properties(local)
+    out = {"rank": rank, "local_rank": local, "hip_device": local,
+           "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid),
+           "pid": os.getpid(), "host": os.uname().nodename}
+    if group is not None:
+        try:
+            out.update({f"group_{k}": v for k, v in group.info().items()})
+        except Exception as e:  # pragma: no cover - reported; the check below fails on it
+            out["group_info_error"] = str(e)[-200:]
+    return out
+
+
+def topology_check(ranks: list[dict], world: int, rccl_library: str | None, transport: str,
+                   rehearsal: bool) -> dict:
+    """The N > 1 record's self-check: N distinct GPUs (PCI address and UUID),
+    the group's transport counting N ranks, and each rank's communicator on
+    the rank's own device.  In a rehearsal the ranks share one GPU by design:
+    distinctness is reported, not required."""
+    pcis = {(r["host"], r["pci"]) for r in ranks}
+    uuids = {(r["host"], r["uuid"]) for r in ranks}
+    distinct = len(pcis) == world and len(uuids) == world
+    counts = [r.get("group_comm_count") for r in ranks]
+    count_ok = all(c == world for c in counts)
+    dev_ok = all(r.get("group_comm_device") == r["hip_device"] for r in ranks)
+    ok = count_ok and dev_ok and (distinct or rehearsal)
+    return {"ranks": ranks, "distinct_gpus": distinct, "group_comm_count_ok": count_ok,
+            "group_comm_device_ok": dev_ok, "group_transport": transport, "rccl_library": rccl_library,
+            "ok": ok, "rehearsal": rehearsal}
 
 
 # Issue classes of one trial of K1's j-loop (4,839 VALU instructions, read from
@@ -679,21 +744,29 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
-    from mpi_blockchain_amd.shard import RcclGroup, ShardedMiner
+    from mpi_blockchain_amd.shard import RcclGroup, ShardedMiner, rccl_path
 
-    miner = GpuMiner(local)
     rehearsal = os.environ.get("BENCH_REHEARSAL") == "1"
+    # A rehearsal (ranks sharing one GPU; tests only) runs the same pow_group
+    # rounds with the all-reduce either over gloo (pow_group_init_custom;
+    # BENCH_REHEARSAL_TRANSPORT=gloo, the default) or through pow_group_init's
+    # RCCL leg with the test library's shared-memory stand-in for RCCL
+    # (rccl_stub: tests/stub_rccl): RCCL itself refuses two ranks on one GPU.
+    transport = os.environ.get("BENCH_REHEARSAL_TRANSPORT", "gloo") if rehearsal else "rccl"
+    if transport == "rccl_stub":
+        from mpi_blockchain_amd.build import STUB_LIB
+
+        os.environ["POW_TEST_RCCL_LIB"] = STUB_LIB
+    miner = GpuMiner(local, test_hooks=transport == "rccl_stub")
     # The library's own RCCL communicator (the id travels over torch.distributed);
-    # at N = 1 a one-rank group, used only by the group_search measurement.  A
-    # rehearsal (ranks sharing one GPU) runs the same pow_group rounds with the
-    # all-reduce over gloo (pow_group_init_custom): RCCL refuses two ranks on one GPU.
+    # at N = 1 a one-rank group, used only by the group_search measurement.
     group, group_err = None, None
-    if rehearsal:
+    if transport == "gloo":
         group = ShardedMiner(miner, rank, world)
     else:
         try:
             group = RcclGroup.from_torch(miner) if dist is not None else \
-                RcclGroup(miner, 0, 1, RcclGroup.make_unique_id())
+                RcclGroup(miner, 0, 1, RcclGroup.make_unique_id(miner.L))
         except Exception as e:  # fatal at N > 1 (below); at N = 1 only group_search is lost, said in group_error
             group_err = f"pow_group_init failed ({e})"
             group = None
@@ -706,12 +779,32 @@ def main():
                 group.close()
                 group = None
                 group_err = "pow_group_init failed on a peer rank"
-        err = native_group_error(group, group_err, world, rehearsal)
+        err = native_group_error(group, group_err, world, transport == "gloo")
         if err:  # fail loudly: no N > 1 number without the native collectives
             print(json.dumps({"error": "bench.py: no native pow_group at N > 1", "group_error": err, "rank": rank}),
                   file=sys.stderr, flush=True)
             dist.destroy_process_group()
             sys.exit(3)
+    # Who took part: every rank's GPU (PCI address, UUID) and the group's own
+    # count of ranks (RCCL: ncclCommCount), gathered before anything is timed.
+    # At N > 1 a record that cannot show N distinct GPUs under one N-rank
+    # communicator is not measured: every rank exits non-zero.
+    topo_ranks = [rank_topology(rank, local, group)]
+    if dist is not None:
+        topo_ranks = [None] * world
+        dist.all_gather_object(topo_ranks, rank_topology(rank, local, group))
+    rlib = None
+    if transport != "gloo":
+        try:
+            rlib = rccl_path(miner.L)
+        except Exception as e:  # pragma: no cover
+            rlib = f"unknown ({e})"
+    topology = topology_check(topo_ranks, world, rlib, transport, rehearsal)
+    if world > 1 and not topology["ok"]:
+        print(json.dumps({"error": "bench.py: topology check failed at N > 1", "topology": topology, "rank": rank}),
+              file=sys.stderr, flush=True)
+        dist.destroy_process_group()
+        sys.exit(4)
     info = miner.device_info()
     tmpl = s0_block()
     d = args.difficulty
@@ -775,6 +868,13 @@ def main():
             gsearch = group_search(group, rank, world)
         except Exception as e:  # pragma: no cover - reported, not fatal: the headline is measured
             gsearch = {"error": str(e)[-300:]}
+        # A winner that does not verify (identical verdict on every rank: all-reduced)
+        # makes an N > 1 record unusable: exit non-zero like a missing group.
+        if world > 1 and "verified" in gsearch and not gsearch["verified"]["ok"]:
+            print(json.dumps({"error": "bench.py: group_search winners failed verification",
+                              "verified": gsearch["verified"], "rank": rank}), file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(5)
     # Config 5 on this job's GPUs: rank 0 launches the MPI job once every
     # other bench rank has exited (their processes release the GPUs, so each
     # GPU carries one pow_node rank and at most bench rank 0 besides).
@@ -794,7 +894,10 @@ def main():
         gone = wait_for_exit(pids[1:], timeout=120)
         proto = protocol_job(world) if gone else {"skipped": "bench ranks 1..N-1 did not exit within 120 s"}
     collective = ("gloo all_reduce(min,sum) per step via pow_group_allreduce_u64 (pow_group_init_custom; "
-                  "rehearsal: ranks share one GPU)" if rehearsal and group is not None else
+                  "rehearsal: ranks share one GPU)" if transport == "gloo" and rehearsal and group is not None else
+                  "stand-in RCCL (tests/stub_rccl, shared memory) all_reduce(min,sum) per step via "
+                  "pow_group_allreduce_u64 (pow_group_init; rehearsal: ranks share one GPU)"
+                  if transport == "rccl_stub" and group is not None else
                   "rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if group is not None and world > 1
                   else f"{dist.get_backend()} all_reduce(min,sum) per step via torch.distributed" if dist is not None
                   else "none (single process)")
@@ -837,6 +940,7 @@ def main():
             checked[str(r)] = {"solutions": n_r, "expected": want["count"],
                                "ok": n_r == want["count"] and mn_r == r * WINDOW + want["first"][0],
                                "fingerprint_ok": fp_r == want["sha256_le_u32"]}
+    parity["unchecked_ranks"] = [r for r in range(world) if str(r) not in checked]
     if checked:
         parity["checked_ranks"] = checked
         parity["count_ok"] = all(c["ok"] for c in checked.values())
@@ -866,6 +970,7 @@ def main():
                                    info["cu_count"]),
         "device": info,
         "parity": parity,
+        "topology": topology,
     }
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline()

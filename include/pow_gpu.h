@@ -95,10 +95,15 @@ const char* pow_last_error(void);
 int pow_get_stats(const pow_ctx* ctx, pow_stats* out);
 /* How the context launches its latency-bound kernels (the one-block hash of
  * pow_hash_block and the first sub-round of pow_mine[_any]):
- * POW_LAUNCH_DIRECT = AQL packets into a queue of its own (no HIP launch call
- * on the path), POW_LAUNCH_HIP = hipLaunchKernel on the context's stream (the
- * fallback when the direct queue cannot be set up; same kernels, same
- * results, ~8 us more per launch).  < 0 = error. */
+ * POW_LAUNCH_HIP = hipLaunchKernel on the context's stream, the shipped
+ * library's only path; POW_LAUNCH_DIRECT = AQL packets into the process's
+ * shared per-device queue (no barrier bit; the test library with POW_AQL=1,
+ * for the dispatch A/B and the ordering tests).  Same kernels, same results.
+ * Every host wait on a launch is bounded (watchdog): a launch that has not
+ * published its result by its deadline (10 s for the latency launches,
+ * 10 s + 2 ns per counter for a throughput launch) fails the call with
+ * POW_EHIP and a diagnostic in pow_last_error(); the context must then not be
+ * reused.  < 0 = error. */
 enum { POW_LAUNCH_HIP = 0, POW_LAUNCH_DIRECT = 1 };
 int pow_launch_path(const pow_ctx* ctx);
 /* Device properties the roofline uses: CU count and peak engine clock (kHz). */
@@ -279,6 +284,18 @@ typedef int (*pow_group_reduce_fn)(void* user, uint64_t* vals, size_t n, int op)
 int pow_group_init_custom(pow_ctx* ctx, int nranks, int rank, pow_group_reduce_fn reduce, void* user,
                           const char* board_name, pow_group** out);
 void pow_group_destroy(pow_group* g);
+/* The group as its transport sees it: *comm_count = the ranks in RCCL's
+ * communicator (ncclCommCount) and *comm_device = its HIP device
+ * (ncclCommCuDevice); for a custom group, nranks (every rank joined) and the
+ * ctx's device (-1 without one).  Either pointer may be NULL.  The scaling
+ * bench records both per rank to show that N distinct GPUs took part. */
+int pow_group_info(const pow_group* g, int* comm_count, int* comm_device);
+/* The file of the RCCL library pow_group_* use (loaded at the first call of
+ * any pow_group_* that needs RCCL; no GPU work): the copy another library of
+ * the process had already loaded (torch's librccl.so) if there is one, else
+ * librccl.so.1 from the library search path.  POW_ECOMM if RCCL cannot be
+ * loaded. */
+int pow_group_rccl_path(char* path, size_t cap);
 /* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream. */
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);
 /* On one node the ranks also share a stop board (named after the id, opened

@@ -28,6 +28,7 @@
 // sharing one GPU, which RCCL refuses).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <link.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -41,15 +42,30 @@
 
 namespace {
 
-// The RCCL entry points used here (rccl.h:187, 220, 260, 339, 611).
+// The RCCL entry points used here (rccl.h:187, 220, 260, 339, 378, 389, 611).
 struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
-  char why[256] = {0};  // non-empty: RCCL is unusable
+  decltype(&ncclCommCount) comm_count = nullptr;
+  decltype(&ncclCommCuDevice) comm_cu_device = nullptr;
+  char why[256] = {0};   // non-empty: RCCL is unusable
+  char path[512] = {0};  // the file the entry points come from
 };
+
+// An RCCL the process has already loaded (torch's libtorch_hip pulls in its
+// own torch/lib/librccl.so at import): its path, or "" if none.
+int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* data) {
+  const char* name = info->dlpi_name;
+  if (!name || !*name) return 0;
+  const char* base = strrchr(name, '/');
+  base = base ? base + 1 : name;
+  if (strncmp(base, "librccl.so", 10) != 0) return 0;
+  snprintf(static_cast<char*>(data), 512, "%s", name);
+  return 1;
+}
 
 const Rccl& rccl() {
   static const Rccl r = [] {
@@ -66,6 +82,13 @@ const Rccl& rccl() {
       }
     }
 #endif
+    // One RCCL runtime per process: if one is loaded already (torch's, in
+    // bench.py's ranks), bind to that very copy (RTLD_NOLOAD: no second
+    // load) instead of resolving librccl.so.1 on our own, which could map
+    // /opt/rocm's copy beside torch's and run two RCCL runtimes side by side.
+    char loaded[512] = {0};
+    if (!h && dl_iterate_phdr(find_loaded_rccl, loaded) && loaded[0])
+      h = dlopen(loaded, RTLD_NOW | RTLD_NOLOAD | RTLD_LOCAL);
     for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
       if (h || (h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
     if (!h) {
@@ -77,8 +100,18 @@ const Rccl& rccl() {
     x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
     x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
-    if (!x.get_unique_id || !x.comm_init_rank || !x.comm_destroy || !x.all_reduce || !x.error_string)
+    x.comm_count = (decltype(x.comm_count))dlsym(h, "ncclCommCount");
+    x.comm_cu_device = (decltype(x.comm_cu_device))dlsym(h, "ncclCommCuDevice");
+    if (!x.get_unique_id || !x.comm_init_rank || !x.comm_destroy || !x.all_reduce || !x.error_string ||
+        !x.comm_count || !x.comm_cu_device)
       snprintf(x.why, sizeof x.why, "RCCL lacks an entry point");
+    Dl_info info;
+    if (x.all_reduce && dladdr((const void*)x.all_reduce, &info) && info.dli_fname) {
+      // dladdr names the object as it was loaded; resolve it to a canonical path
+      char* real = realpath(info.dli_fname, nullptr);
+      snprintf(x.path, sizeof x.path, "%s", real ? real : info.dli_fname);
+      free(real);
+    }
     return x;
   }();
   return r;
@@ -342,6 +375,28 @@ void pow_group_destroy(pow_group* g) {
   if (g->d_buf) (void)hipFree(g->d_buf);
   if (g->h_buf) (void)hipHostFree(g->h_buf);
   delete g;
+}
+
+int pow_group_rccl_path(char* path, size_t cap) {
+  if (!path || !cap) return pow_set_error(POW_EINVAL, "null path");
+  path[0] = 0;
+  const Rccl& R = rccl();
+  if (R.why[0]) return pow_set_error(POW_ECOMM, R.why);
+  snprintf(path, cap, "%s", R.path);
+  return POW_OK;
+}
+
+int pow_group_info(const pow_group* g, int* comm_count, int* comm_device) {
+  if (!g) return pow_set_error(POW_EINVAL, "null group");
+  int n = g->nranks, dev = g->ctx ? pow_ctx_device(g->ctx) : -1;
+  if (g->comm) {  // RCCL's own view of the communicator
+    ncclResult_t r = rccl().comm_count(g->comm, &n);
+    if (r != ncclSuccess) return comm_fail("ncclCommCount", r);
+    if ((r = rccl().comm_cu_device(g->comm, &dev)) != ncclSuccess) return comm_fail("ncclCommCuDevice", r);
+  }
+  if (comm_count) *comm_count = n;
+  if (comm_device) *comm_device = dev;
+  return POW_OK;
 }
 
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op) {

@@ -113,6 +113,11 @@ __device__ __forceinline__ void const_chunk_lds(St& t, const uint32_t* lkw) {
 #define POW_LAT_PIPE 0
 #endif
 // K2' (one block, one wave) runs its 5 chunks through the same helper (NC = 5).
+// The read and its wait are two asm statements: the compiler does not track
+// loads issued from inline asm, so nothing stops it from placing a copy of q
+// between them.  tests/test_build.py (test_asm_lds_reads_waited_before_use)
+// checks on the generated code that no instruction touches an in-flight read's
+// registers before its lgkmcnt(0) wait.
 template <int NC = 4>
 __device__ __forceinline__ void const_chunks_lds_pipelined(uint32_t H[8], St& t, const uint32_t* lk) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -840,9 +845,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
 // (validate_block_for_chain, node.cpp:199-253), so the latency of one hash is
 // what counts.  One wave; the host expands the five chunks' message schedules
 // (K folded in, as pow_build_consts does for K1's chunks 1-4) and passes the
-// 320 K+W words by value in the kernarg segment, which the wave reads with
-// scalar loads issued ahead of their rounds: no H2D copy, no LDS, no barrier,
-// only the 320 compression rounds (the digest's chained part) on the GPU.  The
+// 320 K+W words by value in the kernarg segment, which the wave copies into
+// LDS (one vector load per lane, then a barrier) and reads back 16 B at a time
+// one round group ahead of use: no H2D copy, only the 320 compression rounds
+// (the digest's chained part) on the GPU.  The
 // digest, its duration and a done word go into mapped host memory (no D2H
 // copy, no completion-signal wait).  One wave alone issues a VALU instruction
 // every ~4 cycles whether it is full or half rate (MI355X_MICROARCH.md,

@@ -157,7 +157,8 @@ struct PowResult {
 // K2' (pow_hash_block's one-block path): the five chunks' K[i] + W[i] words of
 // the padded 320-byte message (the message schedule, expanded on the host as
 // pow_build_consts does for K1's chunks 1-4), passed by value (kernarg: no H2D
-// copy, read by scalar loads) ...
+// copy; the wave copies it into LDS with one vector load per lane and a
+// barrier, then reads it 16 B at a time ahead of each round group) ...
 struct PowMsg {
   uint32_t kw[5][64];
 };

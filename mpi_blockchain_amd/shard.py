@@ -87,6 +87,14 @@ class _Group:
             return None
         return MineResult(out, ctr.value, hashes.value, m.stats()["kernel_ms"])
 
+    def info(self) -> dict:
+        """The group as its transport sees it (pow_group_info): RCCL's
+        ncclCommCount and ncclCommCuDevice for an RcclGroup; nranks and the
+        miner's device for a custom group."""
+        n, dev = ctypes.c_int(), ctypes.c_int()
+        check(self.L.pow_group_info(self.g, ctypes.byref(n), ctypes.byref(dev)), self.L)
+        return {"comm_count": n.value, "comm_device": dev.value}
+
     def close(self) -> None:
         if self.g:
             self.L.pow_group_destroy(self.g)
@@ -144,6 +152,28 @@ class RcclGroup(_Group):
         if isinstance(obj[0], str):
             raise RuntimeError(obj[0])
         return cls(miner, dist.get_rank(group), dist.get_world_size(group), obj[0])
+
+
+def rccl_path(L: ctypes.CDLL | None = None) -> str:
+    """The RCCL library file pow_group_* bind to (pow_group_rccl_path): the
+    copy the process already loaded (torch's) if any."""
+    L = L or load()
+    buf = ctypes.create_string_buffer(4096)
+    check(L.pow_group_rccl_path(buf, len(buf)), L)
+    return buf.value.decode()
+
+
+def loaded_rccl_files() -> list[str]:
+    """Every librccl file mapped into this process (/proc/self/maps)."""
+    out = []
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and os.path.basename(parts[-1]).startswith("librccl.so"):
+                p = os.path.realpath(parts[-1])
+                if p not in out:
+                    out.append(p)
+    return out
 
 
 def torch_reduction(device=None, group=None):

@@ -1,6 +1,6 @@
-// TEST INFRASTRUCTURE ONLY: a stand-in for the five RCCL entry points that
+// TEST INFRASTRUCTURE ONLY: a stand-in for the seven RCCL entry points that
 // mpi_blockchain_amd/csrc/pow_group.cpp dlopens (rccl.h:187, 220, 260, 339,
-// 611), reducing over POSIX shared memory instead of xGMI.
+// 378, 389, 611), reducing over POSIX shared memory instead of xGMI.
 //
 // RCCL refuses two ranks on one GPU, and a test box has one GPU, so
 // pow_group_init's RCCL leg (the board opened before ncclCommInitRank and
@@ -68,6 +68,7 @@ void shm_name(const ncclUniqueId& id, char out[48]) {
 struct ncclComm {
   Shared* sh = nullptr;
   int nranks = 0, rank = 0;
+  int device = -1;  // the HIP device current at ncclCommInitRank (as RCCL binds it)
 };
 
 namespace {
@@ -127,6 +128,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
   c->sh = (Shared*)p;  // a fresh object is zero-filled: all counters 0
   c->nranks = nranks;
   c->rank = rank;
+  if (hipGetDevice(&c->device) != hipSuccess) c->device = -1;
   // As RCCL: return once every rank has joined.
   c->sh->joined.fetch_add(1, std::memory_order_acq_rel);
   const double t0 = now_s();
@@ -147,6 +149,18 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
   munmap(comm->sh, sizeof(Shared));
   delete comm;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  if (!comm || !count) return ncclInvalidArgument;
+  *count = comm->nranks;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+  if (!comm || !device) return ncclInvalidArgument;
+  *device = comm->device;
   return ncclSuccess;
 }
 

@@ -71,30 +71,48 @@ def test_valu_microbench_ceilings():
     assert L.pow_valu_rate(0, 7, ctypes.byref(ValuResult())) < 0
 
 
-def run_rehearsal(n: int) -> dict:
+def run_rehearsal(n: int, transport: str = "gloo") -> dict:
     """bench.py as the driver launches it for N > 1 (torch.distributed.run,
-    one rank per GPU), rehearsed with n ranks sharing this box's GPU over gloo
-    (BENCH_REHEARSAL=1; RCCL refuses two ranks on one device)."""
+    one rank per GPU), rehearsed with n ranks sharing this box's GPU
+    (BENCH_REHEARSAL=1; RCCL refuses two ranks on one device).  transport:
+    "gloo" (pow_group_init_custom over gloo) or "rccl_stub" (pow_group_init's
+    RCCL leg with the test library's shared-memory stand-in for RCCL)."""
     import socket
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, BENCH_REHEARSAL="1")
+    env = dict(os.environ, BENCH_REHEARSAL="1", BENCH_REHEARSAL_TRANSPORT=transport)
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                         "--master-addr", "127.0.0.1", "--master-port", str(port),
                         os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "1", "--warmup", "1"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+                       capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 1e9
-    assert "gloo all_reduce" in d["config"]["parallelism"] and "pow_group_init_custom" in d["config"]["parallelism"]
-    # config 4's cooperative search ran through pow_group's C++ rounds on every rank
+    if transport == "gloo":
+        assert "gloo all_reduce" in d["config"]["parallelism"] and "pow_group_init_custom" in d["config"]["parallelism"]
+    else:
+        assert "stand-in RCCL" in d["config"]["parallelism"] and "pow_group_init;" in d["config"]["parallelism"]
+    # config 4's cooperative search ran through pow_group's C++ rounds on every
+    # rank, and every winner verified (digest, difficulty, range, agreement)
     gs = d["group_search"]
     assert gs["n_gpus"] == n and gs["templates"] == 21 and gs["hashes_all_ranks_mean"] > 0, gs
+    assert gs["verified"]["ok"] is True and gs["verified"]["winners_checked"] == 21, gs["verified"]
+    assert all(c is not None for c in gs["counters"]), gs
+    # the topology block: every rank, the group's own rank count (the stand-in's
+    # ncclCommCount), each communicator on its rank's device; one GPU shared
+    topo = d["topology"]
+    assert [r["rank"] for r in topo["ranks"]] == list(range(n)), topo
+    assert all(r["group_comm_count"] == n for r in topo["ranks"]), topo
+    assert topo["group_comm_count_ok"] and topo["group_comm_device_ok"] and topo["ok"], topo
+    assert topo["rehearsal"] is True and topo["distinct_gpus"] is False, topo  # n ranks, one GPU
+    assert topo["group_transport"] == transport
+    if transport == "rccl_stub":
+        assert topo["rccl_library"].endswith("tests/stub_rccl/libstub_rccl.so"), topo
     assert "cpu_baseline" not in d and "ladder" not in d  # rank-0-at-N=1-only extras
     # config 5 at the job's size: mpiexec -np n pow_node (here all on the one GPU)
     pr = d["protocol"]
@@ -108,19 +126,26 @@ def run_rehearsal(n: int) -> dict:
 
 def test_bench_multi_rank_rehearsal():
     """2 ranks: rank 0 prints ONE JSON line with n_gpus = 2, the whole-job
-    value, and rank 0's window checked against its fingerprints."""
+    value, and both ranks' windows checked against their fingerprints."""
     d = run_rehearsal(2)
-    assert d["parity"]["checked_ranks"]["0"]["ok"] is True and d["parity"]["count_ok"] is True
-
-
-@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "tests", "golden",
-                                                    "fingerprints_2p32_S0_at30064771072.json")),
-                    reason="rank-7 window fingerprints not generated")
-def test_bench_eight_rank_rehearsal():
-    """The driver's 8-GPU launch shape (8 ranks; here sharing one GPU): every
-    rank sweeps its own 2^32 window, the job total is the sum, and rank 7's
-    window [7*2^32, 8*2^32) matches the CPU restatement's fingerprints."""
-    d = run_rehearsal(8)
     chk = d["parity"]["checked_ranks"]
-    assert chk["0"]["ok"] is True and chk["7"]["ok"] is True and d["parity"]["count_ok"] is True
+    assert d["parity"]["unchecked_ranks"] == [] and d["parity"]["count_ok"] is True, d["parity"]
+    assert all(chk[str(r)]["ok"] and chk[str(r)]["fingerprint_ok"] for r in range(2)), chk
+
+
+FAR = [os.path.join(ROOT, "tests", "golden", f"fingerprints_2p32_S0_at{r << 32}.json") for r in range(1, 8)]
+
+
+@pytest.mark.skipif(not all(os.path.exists(f) for f in FAR), reason="windows 1..7 fingerprints not all generated")
+def test_bench_eight_rank_rehearsal():
+    """The driver's 8-GPU launch shape (8 ranks; here sharing one GPU) over
+    pow_group_init's RCCL leg (the stand-in RCCL): every rank sweeps its own
+    2^32 window, the job total is the sum, and EVERY rank's window
+    [r*2^32, (r+1)*2^32) matches the CPU restatement's fingerprints (count,
+    lowest counter, sha256 of the timed step's sorted device list)."""
+    d = run_rehearsal(8, "rccl_stub")
+    chk = d["parity"]["checked_ranks"]
+    assert sorted(chk, key=int) == [str(r) for r in range(8)] and d["parity"]["unchecked_ranks"] == [], d["parity"]
+    assert all(c["ok"] is True and c["fingerprint_ok"] is True for c in chk.values()), chk
+    assert d["parity"]["count_ok"] is True and d["parity"]["fingerprint_ok"] is True
     assert d["parity"]["solutions_all_ranks"] > 8 * 8_000_000

@@ -233,3 +233,31 @@ def test_native_group_required_at_n_gt_1():
     assert bench.native_group_error(object(), None, 8, False) is None
     assert bench.native_group_error(None, "e", 1, False) is None
     assert bench.native_group_error(None, "e", 8, True) is None
+
+
+def _topo_rank(r, pci, uuid, count, dev=0, host="h"):
+    return {"rank": r, "local_rank": r, "hip_device": dev, "pci": pci, "uuid": uuid, "pid": 100 + r, "host": host,
+            "group_comm_count": count, "group_comm_device": dev}
+
+
+def test_topology_check():
+    """The N > 1 record's self-check (bench.topology_check): N distinct GPUs
+    by PCI address and UUID, the group's transport counting N ranks, each
+    communicator on its rank's device.  A rehearsal (ranks sharing one GPU)
+    reports non-distinct GPUs without failing; a real run fails on it."""
+    good = [_topo_rank(r, f"0000:{r:02x}:00", f"u{r}", 8, dev=r) for r in range(8)]
+    t = bench.topology_check(good, 8, "/x/librccl.so", "rccl", False)
+    assert t["ok"] and t["distinct_gpus"] and t["group_comm_count_ok"] and t["group_comm_device_ok"]
+    shared = [_topo_rank(r, "0000:05:00", "u0", 8) for r in range(8)]
+    assert not bench.topology_check(shared, 8, None, "rccl", False)["ok"]
+    t = bench.topology_check(shared, 8, None, "gloo", True)
+    assert t["ok"] and not t["distinct_gpus"]
+    short = [dict(x, group_comm_count=4) for x in good]  # RCCL saw 4 ranks in an 8-rank job
+    assert not bench.topology_check(short, 8, None, "rccl", False)["ok"]
+    wrongdev = [dict(x, group_comm_device=0) for x in good]  # every communicator on GPU 0
+    assert not bench.topology_check(wrongdev, 8, None, "rccl", False)["ok"]
+    # same PCI address on two hosts is two GPUs
+    two_hosts = [_topo_rank(r, "0000:05:00", "u0", 2, host=f"h{r}") for r in range(2)]
+    assert bench.topology_check(two_hosts, 2, None, "rccl", False)["distinct_gpus"]
+    missing = [{k: v for k, v in x.items() if k != "group_comm_count"} for x in good]
+    assert not bench.topology_check(missing, 8, None, "rccl", False)["ok"]

@@ -298,12 +298,13 @@ def test_direct_dispatch_kernels_take_explicit_args_only(isa):
 
 
 def test_library_embeds_its_code_object():
-    """pow_aql.cpp loads the kernels from the gfx950 code object in the offload
-    bundle of its own .so file: both libraries hold one that names every kernel
-    it dispatches (the same scan as own_code_object)."""
+    """pow_aql.cpp (test library only, POW_AQL=1) loads the kernels from the
+    gfx950 code object in the offload bundle of its own .so file: the test
+    library holds one that names every kernel it dispatches (the same scan as
+    own_code_object)."""
     from mpi_blockchain_amd import _lib
 
-    for path in (_lib.LIB_PATH, _lib.TEST_LIB_PATH):
+    for path in (_lib.TEST_LIB_PATH,):
         data = open(path, "rb").read()
         found = None
         i = data.find(b"__CLANG_OFFLOAD_BUNDLE__")
@@ -321,3 +322,68 @@ def test_library_embeds_its_code_object():
         assert found is not None and found[:4] == b"\x7fELF", path
         for name in AQL_KERNELS:
             assert (name + ".kd").encode() in found, (path, name)
+
+
+def _vgprs(operands: str) -> set:
+    regs = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", operands):
+        regs.update(range(int(a), int(b) + 1))
+    for a in re.findall(r"\bv(\d+)\b", operands):
+        regs.add(int(a))
+    return regs
+
+
+def test_asm_lds_reads_waited_before_use(isa):
+    """const_chunks_lds_pipelined (K2', the consensus-critical pow_hash_block)
+    issues each K+W read as an asm ds_read_b128 one group ahead and waits for
+    it with a separate asm s_waitcnt lgkmcnt(0).  The compiler's waitcnt
+    insertion does not track loads issued from inline asm, so a copy, spill or
+    reuse of the destination VGPRs placed between the two statements would
+    read (or be overwritten by) a load still in flight.  On the generated
+    gfx950 code: between every asm ds_read_b128 and the next lgkmcnt(0) wait,
+    no instruction names any of its four destination VGPRs."""
+    body = kernel_body(isa, "_Z12pow_hash_one")
+    pending, reads, checked = set(), 0, 0
+    in_asm = False
+    for ln in body.splitlines():
+        s = ln.strip()
+        if s.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if s.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not s or s.startswith((";", ".")) or s.endswith(":"):
+            continue
+        op, _, rest = s.partition(" ")
+        rest = rest.split(";")[0]
+        if op == "s_waitcnt" and "lgkmcnt(0)" in rest:
+            pending = set()
+            continue
+        regs = _vgprs(rest)
+        if op == "ds_read_b128" and in_asm:
+            dst = _vgprs(rest.split(",")[0])
+            assert len(dst) == 4, s
+            assert not (pending & regs), f"a second read reuses in-flight registers: {s}"
+            pending |= dst
+            reads += 1
+            continue
+        if pending:
+            checked += 1
+            assert not (pending & regs), f"{s} touches VGPRs of an asm LDS read still in flight"
+    assert reads == 80 and checked > 4000, (reads, checked)  # 5 chunks x 16 groups of 4 K+W words
+
+
+def test_k1_instruction_budget_guard(isa):
+    """K1 stops here (the half-rate instruction mix bounds it at
+    0.58 of the SIMD-32 peak, 0.96 of the mix-adjusted ceiling; no GPU time is
+    spent on it any more).  This guard catches a regression on the CPU: the
+    trial stays at 4,839 VALU instructions (+-1%), of which at most 2,774
+    issue at half rate (v_alignbit_b32, v_add3_u32, or an SGPR operand)."""
+    for variant in ("_Z10pow_searchILi0ELb0E", "_Z10pow_searchILi1ELb0E", "_Z10pow_searchILi2ELb0E"):
+        body = j_loop_body(isa, variant)
+        lines = [ln.strip() for ln in body.splitlines() if re.match(r"\s+v_", ln)]
+        half = [ln for ln in lines if ln.split()[0] in ("v_alignbit_b32", "v_add3_u32")
+                or re.search(r"\bs\d+\b|\bs\[", ln)]
+        assert abs(len(lines) - 4839) <= 48, (variant, len(lines))
+        assert len(half) <= 2774, (variant, len(half))

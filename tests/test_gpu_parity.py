@@ -586,20 +586,22 @@ def test_full_window_2p32_S1(miner, templates, name):
         assert sol.size == lad[d]["count"] and fp(sol) == lad[d]["sha256_le_u32"], d
 
 
-@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "golden",
-                                                    "fingerprints_2p32_S0_at30064771072.json")),
-                    reason="rank-7 window fingerprints not generated")
-def test_full_window_2p32_far(miner, templates):
-    """S0 over [7*2^32, 8*2^32): the window rank 7 sweeps in bench.py's 8-GPU
-    run (nonce[3] = 'G'..'L' instead of 'a'..'e', counters past 2^32 in the launch base).
-    Counts, sha256 of the sorted list (relative counters) and lowest counter
-    at every rung vs the CPU restatement (tests/golden/gen_fingerprints_2p32.py)."""
+@pytest.mark.parametrize("r", range(1, 8))
+def test_full_window_2p32_far(miner, templates, r):
+    """S0 over [r*2^32, (r+1)*2^32), r = 1..7: the window rank r sweeps in
+    bench.py's N-GPU runs (for r = 7, nonce[3] = 'G'..'L' instead of 'a'..'e';
+    counters past 2^32 in the launch base).  Counts, sha256 of the sorted list
+    (relative counters) and lowest counter at every rung vs the CPU
+    restatement (tests/golden/gen_fingerprints_2p32.py; reference's rule
+    block.cpp:91-96)."""
     import json
 
-    start = 7 << 32
-    fps = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
-                                      f"fingerprints_2p32_S0_at{start}.json")))
-    assert fps["start"] == start
+    start = r << 32
+    path = os.path.join(os.path.dirname(__file__), "golden", f"fingerprints_2p32_S0_at{start}.json")
+    if not os.path.exists(path):
+        pytest.skip(f"window {r} fingerprints not generated")
+    fps = json.load(open(path))
+    assert fps["start"] == start and fps["template"] == "S0" and fps["count"] == 1 << 32
     b = block_from_template(templates["S0"])
     lad = fps["ladder"]
     got = miner.sweep(b, start, 1 << 32, 9, cap=9_000_000)

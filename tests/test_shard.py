@@ -55,6 +55,7 @@ def _custom_group_worker(rank, world, port, q):
         # the round consensus word {counter, go, ok}: one rank cancelled
         out["consensus"] = g.allreduce([U64MAX if rank else 12345, 0 if rank == world - 1 else 1, 1], "min")
         blk = _lib.Block()
+        out["info"] = g.info()
         out["mine_rc"] = _lib.load().pow_group_mine(g.g, ctypes.byref(blk), 0, 1, 0, 9, None, 0, ctypes.byref(blk),
                                                     None, None)
     q.put((rank, out))
@@ -93,6 +94,7 @@ def test_custom_group_collectives(world):
         assert out[r]["sum"] == want_sum
         assert out[r]["consensus"] == [12345, 0, 1]
         assert out[r]["mine_rc"] == _lib.POW_EINVAL
+        assert out[r]["info"] == {"comm_count": world, "comm_device": -1}  # no context: no device
 
 
 def test_custom_group_rank_count_mismatch():
@@ -119,6 +121,46 @@ def test_custom_group_rank_count_mismatch():
     assert L.pow_group_init_custom(None, 1, 0, fail, None, None, ctypes.byref(g)) == _lib.POW_ECOMM and not g
     assert L.pow_group_init_custom(None, 1, 0, _lib.REDUCE_FN(), None, None, ctypes.byref(g)) == _lib.POW_EINVAL
     assert L.pow_group_init_custom(None, 1, 1, fn, None, None, ctypes.byref(g)) == _lib.POW_EINVAL
+
+
+_RCCL_PROBE = r"""
+import ctypes, json, sys
+from mpi_blockchain_amd import _lib
+from mpi_blockchain_amd.shard import loaded_rccl_files, rccl_path
+if sys.argv[1] == "torch":  # _lib.load imports torch first (libtorch_hip loads torch/lib/librccl.so)
+    libs = [_lib.load(), _lib.load(test_hooks=True)]
+else:  # a C caller without torch: the bare libraries
+    libs = [ctypes.CDLL(_lib.LIB_PATH), ctypes.CDLL(_lib.TEST_LIB_PATH)]
+    for L in libs:
+        L.pow_group_rccl_path.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+before = loaded_rccl_files()
+out = {"before": before, "shipped": rccl_path(libs[0]), "test": rccl_path(libs[1]), "after": loaded_rccl_files(),
+       "torch": "torch" in sys.modules}
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("first", ["torch", "alone"])
+def test_group_binds_the_loaded_rccl(first):
+    """One RCCL runtime per process: pow_group binds the copy the process has
+    already loaded (torch's torch/lib/librccl.so, which libtorch_hip pulls in
+    at import) instead of mapping /opt/rocm's beside it; a process without
+    one loads librccl.so.1 from the search path.  Both libraries agree, and
+    exactly one librccl file is mapped afterwards.  No GPU needed."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _RCCL_PROBE, first], cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["shipped"] == out["test"] and out["after"] == [out["shipped"]], out
+    if first == "torch":
+        assert out["torch"] and out["before"] == [out["shipped"]] and "/torch/lib/" in out["shipped"], out
+    else:
+        assert not out["torch"] and out["before"] == [] and out["shipped"].startswith("/opt/rocm"), out
 
 
 def test_native_partition_matches():

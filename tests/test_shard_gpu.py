@@ -273,7 +273,9 @@ def test_native_group_beside_torch_rccl():
     """bench.py at N > 1 runs torch's nccl (RCCL) process group and the
     library's own RCCL communicator (pow_group, RCCL dlopen'ed) in one
     process: both on this GPU at world size 1, collectives on each, then a
-    group search."""
+    group search.  pow_group binds the RCCL copy torch loaded (one RCCL
+    runtime in the process), and RCCL's own view of the communicator
+    (ncclCommCount, ncclCommCuDevice) is one rank on device 0."""
     import torch
     import torch.distributed as dist
 
@@ -291,7 +293,12 @@ def test_native_group_beside_torch_rccl():
         t = torch.ones(4, device="cuda:0")
         dist.all_reduce(t)
         assert t.sum().item() == 4
+        from mpi_blockchain_amd.shard import loaded_rccl_files, rccl_path
+
         with GpuMiner(0) as m, RcclGroup.from_torch(m) as g:
+            assert g.info() == {"comm_count": 1, "comm_device": 0}
+            files = loaded_rccl_files()
+            assert len(files) == 1 and rccl_path(m.L) == files[0] and "torch" in files[0], (files, rccl_path(m.L))
             assert g.allreduce([9, 2], "min") == [9, 2]
             r = g.mine(make_block(1, 0, 9, 1700000000, b""), 0, 1 << 20, 9)
             assert r is not None and r.counter == 238
