@@ -300,7 +300,7 @@ def validation_latency() -> dict:
         out["calls"] = g["calls"]
         from mpi_blockchain_amd.miner import GpuMiner
 
-        with GpuMiner(0) as m:  # how K2' is launched: "direct" (AQL packet, pow_aql.cpp) or "hip"
+        with GpuMiner(0) as m:  # how K2' is launched: "hip" (hipLaunchKernel; the shipped library's only path)
             out["launch_path"] = m.launch_path()
     except Exception as e:  # pragma: no cover - reported, not fatal
         out["gpu_error"] = str(e)[-300:]
@@ -316,8 +316,17 @@ def validation_latency() -> dict:
                 R.L.ref_block_to_hash_median_ns(ctypes.byref(b), 2000) / 1e3, 2)
     except Exception as e:  # pragma: no cover
         out["reference_error"] = str(e)[-300:]
+    g_us = out.get("pow_hash_block_call_us_median")
+    for flav in ("O0", "O2"):
+        r_us = out.get(f"reference_block_to_hash_{flav}_us_median")
+        if g_us and r_us:
+            out[f"gpu_call_over_reference_{flav}"] = round(g_us / r_us, 2)
     out["note"] = ("one block per call, as validate_block_for_chain checks a received block; GPU: call = "
-                   "AQL packet (launch_path) + kernel + result in mapped host memory; reference: picosha2 + hex on one host core")
+                   "hipLaunchKernel + kernel (one wave, ~4,500 dependent VALU instructions) + result in mapped host "
+                   "memory; reference: picosha2 + hex on one host core.  The GPU call is SLOWER than the reference's "
+                   "block_to_hash (gpu_call_over_reference_O0 / _O2 = how many times the reference's as-shipped "
+                   "-O0 / -O2 time): f3 keeps one authoritative SHA-256 implementation on both sides of the wire, "
+                   "it is not a speed-up")
     return out
 
 

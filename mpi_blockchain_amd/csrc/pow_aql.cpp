@@ -36,10 +36,13 @@
 // free (read index > idx - size), writes the body, stores the 32-bit
 // header+setup word with release semantics, then rings the doorbell with idx.
 // It relies on three statements of hsa.h (ROCm 7.2): every slot starts
-// INVALID and a processed slot is INVALID again ("processed in the past, but
-// not reassigned", hsa.h:2816-2820); a packet processor must not process an
-// INVALID packet (same lines); and on a MULTI queue the doorbell "can be
-// updated with any value" (hsa.h:2343-2346), i.e. out of order.
+// INVALID (hsa.h:2368-2371) and a processed slot is INVALID again ("processed
+// in the past, but not reassigned", hsa.h:2815-2818); a packet processor must
+// not process an INVALID packet (hsa.h:2818-2819); and on a MULTI queue the
+// doorbell "can be updated with any value" (hsa.h:2343-2346), i.e. out of
+// order.  tests/test_gpu_parity.py::test_direct_dispatch_stalled_producer
+// forces the case that matters (a later producer's header and doorbell before
+// an earlier producer's header).
 // Any failure to set this up leaves the caller on the HIP launch path (the
 // same kernels).
 #include <dlfcn.h>
