@@ -679,13 +679,23 @@ int main(int argc, char** argv) {
   Node n(o);
   int gpu_rc = 0;
   std::thread gpu_init;
+  using clk = std::chrono::steady_clock;
+  const auto t_start = clk::now();
+  double gpu_ms = 0;
+  auto timed_init = [&] {
+    const auto t = clk::now();
+    gpu_rc = n.init_gpu();
+    gpu_ms = std::chrono::duration<double, std::milli>(clk::now() - t).count();
+  };
   if (o.serial_init) {
-    if (n.init_gpu() != 0) return 1;
+    timed_init();
+    if (gpu_rc != 0) return 1;
   } else {
-    gpu_init = std::thread([&] { gpu_rc = n.init_gpu(); });
+    gpu_init = std::thread(timed_init);
   }
   int provided = 0;
   const int mpi_rc = MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);
+  const double mpi_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
   if (gpu_init.joinable()) gpu_init.join();
   if (mpi_rc != MPI_SUCCESS) {
     fprintf(stderr, "Error de MPI al inicializar.\n");
@@ -701,6 +711,19 @@ int main(int argc, char** argv) {
   // One start line for every rank (see the header): GPU set-up ended at a
   // different time on each rank.  With --serial-init, MPI_Init was it.
   if (!o.serial_init) MPI_Barrier(MPI_COMM_WORLD);
+#ifdef POW_NODE_TEST_KNOBS
+  // Start-up split (test build only, stderr): where a slow network's first
+  // second goes (GPU set-up: HIP runtime + two contexts + warm-up; MPI_Init).
+  {
+    int r = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &r);
+    fprintf(stderr, "[%d] start-up: gpu set-up %.1f ms, MPI_Init %.1f ms, start line at %.1f ms\n", r, gpu_ms, mpi_ms,
+            std::chrono::duration<double, std::milli>(clk::now() - t_start).count());
+  }
+#else
+  (void)gpu_ms;
+  (void)mpi_ms;
+#endif
   n.run();
   MPI_Finalize();
   return 0;

@@ -46,6 +46,9 @@ def main() -> int:
     ap.add_argument("--mutual", action="store_true",
                     help="--private-lead 3, as tests/test_node_gpu.py::test_mutual_chain_request: every rank "
                          "must lose by several blocks and splice a peer's chain (find = 2)")
+    ap.add_argument("--slow-s", type=float, default=3.0,
+                    help="with POW_NODE_LOG_DIR set, keep the output of every run slower than this")
+    ap.add_argument("--keep-all", action="store_true", help="with POW_NODE_LOG_DIR set, keep every run's output")
     a = ap.parse_args()
     extra = ("--hold-first", "1") if a.forced_fork else ("--winner-pause-us", "400", "--pause-us", "200")
     if a.mutual:
@@ -73,6 +76,13 @@ def main() -> int:
                 ok = False
         ok = ok and complete > 0
         n_fork = sum(run.stdout.count(m) for m in FORK_MSGS)
+        # a slow network (or any, with --keep-all) keeps its whole output, start-up split included
+        keep = os.environ.get("POW_NODE_LOG_DIR")
+        if keep and (wall > a.slow_s or a.keep_all):
+            os.makedirs(keep, exist_ok=True)
+            with open(os.path.join(keep, f"soak_run{i + 1}_wall{wall:.2f}s.log"), "w") as f:
+                f.write(f"rc {run.returncode} wall {wall:.3f} s\n{run.stdout}")
+        startup = re.findall(r"start line at ([0-9.]+) ms", run.stdout)
         if a.forced_fork:
             ok = ok and n_fork >= 1
         if a.mutual:
@@ -88,7 +98,9 @@ def main() -> int:
         forks += n_fork
         walls.append(wall)
         print(f"run {i + 1}/{a.runs}: rc {run.returncode} wall {wall:.2f} s, dumps {len(run.chains)}, "
-              f"complete {complete}, fork-path lines {n_fork}{cross} -> {'ok' if ok else 'FAIL'}", flush=True)
+              f"complete {complete}, fork-path lines {n_fork}{cross}"
+              f"{', start line ' + max(startup, key=float) + ' ms' if startup else ''} -> {'ok' if ok else 'FAIL'}",
+              flush=True)
         if not ok:
             print(run.stdout[-6000:])
             return 1
