@@ -28,7 +28,7 @@ build)
     -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer \
     -DPOW_TEST_HOOKS -I "$R/include" -I "$C" \
     "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
-    "$C/valu_peak.hip" "$C/pow_aql.cpp" -o "$O/libpow_gpu.so" -L /opt/rocm/lib -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
+    "$C/valu_peak.hip" "$C/pow_aql.cpp" "$C/pow_test_kernels.hip" -o "$O/libpow_gpu.so" -L /opt/rocm/lib -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
   $CLANG -std=c11 -O1 -g $SAN -I "$R/include" "$R/examples/mine_chain.c" \
     -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/mine_chain"
   $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g $SAN -pthread -I "$R/include" "$R/examples/board_two_ctx.c" \
@@ -66,6 +66,11 @@ run)
   /opt/conda/bin/mpiexec -np 2 "$O/pow_node" --difficulty 9 --serial-init 1 --private-lead 3 > net_mutual.log
   cat net_mutual.log
   echo "chains (mutual requests):"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
+  rm -f ./*.out
+  # the same 4-rank mutual case with the test library's direct AQL dispatch (POW_AQL=1)
+  POW_AQL=1 /opt/conda/bin/mpiexec -np 4 "$O/pow_node" --difficulty 9 --serial-init 1 --private-lead 3 > net_mutual_aql.log
+  cat net_mutual_aql.log
+  echo "chains (mutual requests, direct dispatch):"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   ;;
 tsan-build)
   # ThreadSanitizer on pow_node's own code (receive thread, miner thread, GPU
@@ -78,7 +83,7 @@ tsan-build)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -fPIC -shared -std=c++17 -mcode-object-version=5 \
     -Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer -DPOW_TEST_HOOKS -I "$R/include" -I "$C" \
     "$C/pow_api.cpp" "$C/pow_board.cpp" "$C/pow_group.cpp" "$C/pow_kernels.hip" "$C/pow_sort.hip" \
-    "$C/valu_peak.hip" "$C/pow_aql.cpp" -o "$T/libpow_gpu.so" -L /opt/rocm/lib -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
+    "$C/valu_peak.hip" "$C/pow_aql.cpp" "$C/pow_test_kernels.hip" -o "$T/libpow_gpu.so" -L /opt/rocm/lib -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
   $CLANGXX -std=c++17 -O1 -g -fsanitize=thread -pthread -DPOW_NODE_TEST_KNOBS -I "$R/include" -I "$MPI_INC" \
     "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$T" -lpow_gpu \
     -Wl,-rpath,'$ORIGIN' "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$T/pow_node_tsan"
@@ -110,6 +115,10 @@ tsan-run)
   /opt/conda/bin/mpiexec -np 2 "$T/pow_node_tsan" --difficulty 9 --private-lead 3 > net_mutual.log
   cat net_mutual.log
   echo "chains (mutual requests):"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
+  rm -f ./*.out
+  POW_AQL=1 /opt/conda/bin/mpiexec -np 4 "$T/pow_node_tsan" --difficulty 9 --private-lead 3 > net_mutual_aql.log
+  cat net_mutual_aql.log
+  echo "chains (mutual requests, direct dispatch):"; md5sum ./*.out | awk '{print $1}' | sort | uniq -c
   ;;
 *)
   echo "usage: $0 build|run|tsan-build|tsan-run" >&2; exit 2;;
