@@ -118,6 +118,7 @@ def _group_rank(rank, world, port, q, fault_rank, transport="gloo"):
     with GpuMiner(0, test_hooks=stub or rank == fault_rank) as m:
         m.warmup()
         with make_group(m) as sm:
+            out["info"] = sm.info()  # RCCL's (here the stand-in's) ncclCommCount / ncclCommCuDevice
             if fault_rank >= 0:
                 try:
                     sm.mine(S0, 0, 1 << 30, 21)
@@ -188,6 +189,8 @@ def test_group_multiprocess(world, transport):
     from mpi_blockchain_amd.block import nonce_from_counter, solves_problem
 
     out = _run_ranks(world, transport=transport)
+    # the group as its transport sees it: `world` ranks, each communicator on device 0
+    assert all(out[r]["info"] == {"comm_count": world, "comm_device": 0} for r in range(world)), out
     if transport == "rccl_stub":
         for r in range(world):
             assert out[r]["shm_left"] == [], out[r]["shm_left"]
