@@ -277,6 +277,47 @@ int set_dev(const pow_ctx* ctx) {
   return POW_OK;
 }
 
+// Every host wait on the context's stream goes through here (the watchdog):
+// an event recorded behind the queued work is polled until it completes or
+// `deadline_ns` (CLOCK_MONOTONIC) passes.  nap = long waits: 50 us sleeps
+// between polls instead of a spinning core (a protocol rank
+// should not burn a core while its GPU mines; hipEventSynchronize spins,
+// blocking-sync event or not), at most 50 us late on a >= 8 ms launch, with
+// the calling thread's timer slack lowered to 1 us meanwhile (a 50 us sleep
+// otherwise lasts ~100 us: the end of a pow_mine_any launch that found a block
+// at d = 25 was seen 50-75 us late, rocprofv3 HIP trace of tools/ttb_c 25).
+// Past the deadline: POW_EHIP naming `what`, and the context must not be
+// reused (its work may still be queued).  On success a final
+// hipStreamSynchronize returns at once and reports any error of the work.
+int stream_wait(pow_ctx* ctx, const char* what, uint64_t t0, uint64_t deadline_ns, bool nap) {
+  HIP_OK(hipEventRecord(ctx->ev_block, ctx->stream));
+  const int slack = nap ? prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0) : 0;
+  if (slack > 1000) prctl(PR_SET_TIMERSLACK, 1000ul, 0, 0, 0);
+  hipError_t q;
+  bool late = false;
+  for (uint32_t n = 1; (q = hipEventQuery(ctx->ev_block)) == hipErrorNotReady; ++n) {
+    if (nap) std::this_thread::sleep_for(std::chrono::microseconds(POW_WAIT_POLL_US));
+    if ((nap || (n & 255u) == 0) && mono_ns() > deadline_ns) {
+      late = true;
+      break;
+    }
+  }
+  if (slack > 1000) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+  if (late)
+    return fail(POW_EHIP, "%s: watchdog: not complete after %.3f s (deadline %.3f s; hipStreamQuery: %s); "
+                "the context must not be reused",
+                what, (mono_ns() - t0) * 1e-9, (deadline_ns - t0) * 1e-9, hipGetErrorString(hipStreamQuery(ctx->stream)));
+  HIP_OK(q);
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return POW_OK;
+}
+
+// The common case: `what` must be done within the base deadline plus `extra_ns`.
+int stream_wait_for(pow_ctx* ctx, const char* what, uint64_t extra_ns) {
+  const uint64_t t0 = mono_ns();
+  return stream_wait(ctx, what, t0, t0 + ctx->watchdog_ns + extra_ns, false);
+}
+
 // Split [start, start+count) (count <= 2^32) into the kernel's prefix form.
 int make_launch(uint64_t start, uint64_t count, unsigned diff, uint32_t cap, uint32_t mode,
                 PowLaunch* L) {
@@ -333,45 +374,20 @@ int run_search(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, uint
                            ctx->d_res));
   HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_OK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(PowResult), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OK(hipEventRecord(ctx->ev_block, ctx->stream));
-  // The wait is bounded (watchdog): the base deadline plus 2 ns per counter,
-  // i.e. a launch slower than 0.5 G trials/s (1/18 of the chip's rate, e.g.
-  // one GPU shared by many processes) is reported as stuck instead of waited
-  // for forever.
-  // Long launches (>= 2^26 counters, >= 8 ms): poll the event every 50 us
-  // instead of spinning a host core for the whole kernel (a
-  // protocol rank should not burn a core while its GPU mines; hipEvent-
-  // Synchronize spins, blocking-sync event or not).  At most 50 us late on a
-  // >= 8 ms launch.  Short launches spin: their latency is the whole
-  // time-to-block at low difficulty.
-  // The calling thread's timer slack (50 us by default on Linux) is lowered
-  // to 1 us for the wait: a 50 us sleep otherwise lasts ~100 us, and the end
-  // of a pow_mine_any launch that found a block at d = 25 was seen 50-75 us
-  // late (rocprofv3 HIP trace of tools/ttb_c 25).
+  // Bounded wait (watchdog): the base deadline plus 2 ns per counter, i.e. a
+  // launch slower than 0.5 G trials/s (1/18 of the chip's rate, e.g. one GPU
+  // shared by many processes) is reported as stuck instead of waited for
+  // forever.  Long launches (>= 2^26 counters, >= 8 ms) sleep between polls;
+  // short ones spin: their latency is the whole time-to-block at low
+  // difficulty.
   {
-    const bool nap = count >= (1ull << 26);
-    const uint64_t t0 = mono_ns(), deadline = t0 + ctx->watchdog_ns + 2ull * count;
-    const int slack = nap ? prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0) : 0;
-    if (slack > 1000) prctl(PR_SET_TIMERSLACK, 1000ul, 0, 0, 0);
-    hipError_t q;
-    bool late = false;
-    for (uint32_t n = 1; (q = hipEventQuery(ctx->ev_block)) == hipErrorNotReady; ++n) {
-      if (nap) std::this_thread::sleep_for(std::chrono::microseconds(POW_WAIT_POLL_US));
-      if ((nap || (n & 255u) == 0) && mono_ns() > deadline) {
-        late = true;
-        break;
-      }
-    }
-    if (slack > 1000) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
-    if (late)
-      return fail(POW_EHIP,
-                  "search kernel (mode %u, %llu counters from %llu, d = %u): watchdog: not complete after %.3f s "
-                  "(deadline %.3f s; hipStreamQuery: %s); the context must not be reused",
-                  mode, (unsigned long long)count, (unsigned long long)start, diff, (mono_ns() - t0) * 1e-9,
-                  (deadline - t0) * 1e-9, hipGetErrorString(hipStreamQuery(ctx->stream)));
-    HIP_OK(q);
+    char what[160];
+    snprintf(what, sizeof what, "search kernel (mode %u, %llu counters from %llu, d = %u)", mode,
+             (unsigned long long)count, (unsigned long long)start, diff);
+    const uint64_t t0 = mono_ns();
+    if (int rc2 = stream_wait(ctx, what, t0, t0 + ctx->watchdog_ns + 2ull * count, count >= (1ull << 26)))
+      return rc2;
   }
-  HIP_OK(hipStreamSynchronize(ctx->stream));
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats.kernel_ms += ms;
@@ -607,6 +623,9 @@ bool cancel_moved(const volatile uint32_t* cancel_word, uint32_t epoch) {
 int pow_ctx_device(const pow_ctx* ctx) { return ctx->device; }
 void pow_ctx_set_stats(pow_ctx* ctx, const pow_stats& s) { ctx->stats = s; }
 void* pow_ctx_stream(const pow_ctx* ctx) { return (void*)ctx->stream; }
+int pow_ctx_stream_wait(pow_ctx* ctx, const char* what, uint64_t budget_ns) {
+  return stream_wait_for(ctx, what, budget_ns);
+}
 int pow_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 extern "C" {
@@ -720,7 +739,11 @@ int pow_init(int device, pow_ctx** out) {
 void pow_destroy(pow_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  // Bounded too (the base deadline + 10 s): a context whose launch never
+  // completed (a watchdog error) is left allocated rather than freed under a
+  // kernel that may still write it.  (No event: pow_init failed before any
+  // launch, nothing is queued.)
+  if (ctx->stream && ctx->ev_block && stream_wait_for(ctx, "pow_destroy", 10ull * 1000000000ull) != POW_OK) return;
 #ifdef POW_TEST_HOOKS
   pow_aql_close(ctx->aql);
 #endif
@@ -764,7 +787,7 @@ int pow_warmup(pow_ctx* ctx) {
   PowMsg M;
   memset(&M, 0, sizeof M);
   HIP_OK(pow_launch_hash_one(ctx->stream, M, ctx->d_one, 0));  // publishes done = 0: never a live seq
-  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (int rc = stream_wait_for(ctx, "warm-up launches", 0)) return rc;
 #ifdef POW_TEST_HOOKS
   if (ctx->aql) {  // the same launches once through the direct-dispatch queue (its first packets)
     for (int k = 0; k < 9; ++k) {
@@ -900,7 +923,7 @@ int pow_hash_blocks(pow_ctx* ctx, const pow_block* blocks, size_t n, uint8_t* di
   HIP_OK(hipEventRecord(ctx->ev1, ctx->stream));
   std::vector<uint32_t> dg(n * 8);
   HIP_OK(hipMemcpyAsync(dg.data(), ctx->d_dig, n * 32, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (int rc = stream_wait_for(ctx, "batch hash kernel", 100ull * n)) return rc;  // + 100 ns per block
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats = pow_stats{ms, 1u, (uint64_t)n};
@@ -938,7 +961,7 @@ int pow_sweep_device(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, ui
     const uint64_t k = std::min<uint64_t>(ntail, cap32 - nblk);
     HIP_OK(hipMemcpyAsync(dev_out + nblk, ctx->d_tail, k * sizeof(uint32_t), hipMemcpyDeviceToDevice,
                           ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (int rc = stream_wait_for(ctx, "sweep tail copy", 0)) return rc;
   }
   if (n_found) *n_found = nblk + ntail;
   if (min_ctr && ctx->h_res->min_rel != ~0ull) *min_ctr = ctr_start + ctx->h_res->min_rel;
@@ -980,7 +1003,7 @@ int pow_sweep(pow_ctx* ctx, const pow_block* tmpl, uint64_t ctr_start, uint64_t 
     size_t tb = ctx->sort_tmp_bytes;
     HIP_OK(pow_sort_u32(ctx->d_sort_tmp, &tb, ctx->d_out, ctx->d_alt, (uint32_t)got, &sorted, ctx->stream));
     HIP_OK(hipMemcpyAsync(out_ctrs, sorted, got * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (int rc = stream_wait_for(ctx, "sweep sort and copy", 4ull * got)) return rc;  // + 1 ns per byte
   }
   return n > cap ? fail(POW_ENOSPC, "%zu solutions > cap %zu", n, cap) : POW_OK;
 }
@@ -1159,8 +1182,7 @@ int pow_dev_read(pow_ctx* ctx, const void* dev, void* host, size_t bytes) {
   if (!ctx || (bytes && (!dev || !host))) return fail(POW_EINVAL, "null");
   if (int rc = set_dev(ctx)) return rc;
   HIP_OK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OK(hipStreamSynchronize(ctx->stream));
-  return POW_OK;
+  return stream_wait_for(ctx, "device read", bytes);  // + 1 ns per byte
 }
 
 }  // extern "C"

@@ -42,7 +42,7 @@
 
 namespace {
 
-// The RCCL entry points used here (rccl.h:187, 220, 260, 339, 378, 389, 611).
+// The RCCL entry points used here (rccl.h:187, 220, 260, 271, 339, 378, 389, 611).
 struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
@@ -51,6 +51,7 @@ struct Rccl {
   decltype(&ncclGetErrorString) error_string = nullptr;
   decltype(&ncclCommCount) comm_count = nullptr;
   decltype(&ncclCommCuDevice) comm_cu_device = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
   char why[256] = {0};   // non-empty: RCCL is unusable
   char path[512] = {0};  // the file the entry points come from
 };
@@ -102,8 +103,9 @@ const Rccl& rccl() {
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
     x.comm_count = (decltype(x.comm_count))dlsym(h, "ncclCommCount");
     x.comm_cu_device = (decltype(x.comm_cu_device))dlsym(h, "ncclCommCuDevice");
+    x.comm_abort = (decltype(x.comm_abort))dlsym(h, "ncclCommAbort");
     if (!x.get_unique_id || !x.comm_init_rank || !x.comm_destroy || !x.all_reduce || !x.error_string ||
-        !x.comm_count || !x.comm_cu_device)
+        !x.comm_count || !x.comm_cu_device || !x.comm_abort)
       snprintf(x.why, sizeof x.why, "RCCL lacks an entry point");
     Dl_info info;
     if (x.all_reduce && dladdr((const void*)x.all_reduce, &info) && info.dli_fname) {
@@ -143,6 +145,8 @@ struct pow_group {
   uint64_t* h_buf = nullptr;  // pinned host mirror
   pow_board* board = nullptr; // the node's stop board (null: more than 64 ranks, or none available)
   uint32_t searches = 0;      // searches so far: every rank counts the same (the calls are collective)
+  uint64_t shard_budget = 0;  // counters of the current round's largest shard (the all-reduce's watchdog budget)
+  bool broken = false;        // an all-reduce passed its deadline: ncclCommAbort, not ncclCommDestroy
 };
 
 namespace {
@@ -165,7 +169,16 @@ int group_allreduce(pow_group* g, uint64_t* v, size_t n, int op) {
   if (r != ncclSuccess) return comm_fail("ncclAllReduce", r);
   if ((e = hipMemcpyAsync(g->h_buf, g->d_buf, n * 8, hipMemcpyDeviceToHost, st)) != hipSuccess)
     return hip_fail("hipMemcpyAsync", e);
-  if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+  // Bounded (the watchdog): a peer that never joins this all-reduce (dead, or
+  // stuck in its own launch) fails the call instead of hanging every rank.  A
+  // peer still mining its shard of the round is waited for: the budget grows
+  // with the round's shard (2 ns per counter, as the launch watchdog).
+  if (pow_ctx_stream_wait(g->ctx, "ncclAllReduce", 2ull * g->shard_budget) != POW_OK) {
+    g->broken = true;  // the communicator has an operation in flight: destroy aborts it
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s", pow_last_error());
+    return pow_set_error(POW_ECOMM, buf);
+  }
   memcpy(v, g->h_buf, n * sizeof(uint64_t));
   return POW_OK;
 }
@@ -224,6 +237,7 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
     const uint64_t n = std::min(round_size, ctr_count - done);
     uint64_t s = 0, k = 0;
     pow_group_partition(ctr_start + done, n, g->rank, g->nranks, &s, &k);
+    g->shard_budget = n / (uint64_t)g->nranks + 1;  // the largest shard of the round
     // {counter found by this rank (any: its first; lowest: its shard's lowest), go (0 = cancelled), ok (0 = failed)}
     uint64_t v[3] = {UINT64_MAX, 1, 1};
     int local_rc = POW_OK;
@@ -241,7 +255,9 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
       }
     }
     if (cancel_moved(cancel_word, epoch)) v[1] = 0;
-    if (int rc = group_allreduce(g, v, 3, POW_REDUCE_MIN)) return rc;
+    const int arc = group_allreduce(g, v, 3, POW_REDUCE_MIN);
+    g->shard_budget = 0;
+    if (arc) return arc;
     if (hashes_done) *hashes_done = st.s.hashes;
     pow_ctx_set_stats(g->ctx, st.s);
     if (v[2] == 0)  // every rank leaves the search together
@@ -370,7 +386,7 @@ void pow_group_destroy(pow_group* g) {
     (void)hipSetDevice(pow_ctx_device(g->ctx));
     pow_board_bind(g->ctx, nullptr, 0, 0);
   }
-  if (g->comm) (void)rccl().comm_destroy(g->comm);
+  if (g->comm) (void)(g->broken ? rccl().comm_abort(g->comm) : rccl().comm_destroy(g->comm));
   pow_board_close(g->board);
   if (g->d_buf) (void)hipFree(g->d_buf);
   if (g->h_buf) (void)hipHostFree(g->h_buf);

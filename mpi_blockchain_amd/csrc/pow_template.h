@@ -188,6 +188,10 @@ void pow_build_consts(const struct pow_block* tmpl, PowConsts* out);
 // Library-internal accessors of a context (used by pow_group.cpp).
 int pow_ctx_device(const struct pow_ctx* ctx);
 void* pow_ctx_stream(const struct pow_ctx* ctx);  // the ctx's hipStream_t
+// Bounded wait for everything queued on the ctx's stream (the watchdog):
+// POW_OK, or POW_EHIP naming `what` once `budget_ns` past the base deadline
+// has gone by without the stream draining.
+int pow_ctx_stream_wait(struct pow_ctx* ctx, const char* what, uint64_t budget_ns);
 // Record `msg` for pow_last_error(); returns `code`.
 int pow_set_error(int code, const char* msg);
 // True once another thread moved the caller's cancel word off `epoch` (acquire load).

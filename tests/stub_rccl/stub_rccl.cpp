@@ -1,6 +1,6 @@
-// TEST INFRASTRUCTURE ONLY: a stand-in for the seven RCCL entry points that
-// mpi_blockchain_amd/csrc/pow_group.cpp dlopens (rccl.h:187, 220, 260, 339,
-// 378, 389, 611), reducing over POSIX shared memory instead of xGMI.
+// TEST INFRASTRUCTURE ONLY: a stand-in for the eight RCCL entry points that
+// mpi_blockchain_amd/csrc/pow_group.cpp dlopens (rccl.h:187, 220, 260, 271,
+// 339, 378, 389, 611), reducing over POSIX shared memory instead of xGMI.
 //
 // RCCL refuses two ranks on one GPU, and a test box has one GPU, so
 // pow_group_init's RCCL leg (the board opened before ncclCommInitRank and
@@ -151,6 +151,10 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   delete comm;
   return ncclSuccess;
 }
+
+// As RCCL's: tear the communicator down without waiting for operations in
+// flight (the stub has none once a call returns).
+ncclResult_t ncclCommAbort(ncclComm_t comm) { return ncclCommDestroy(comm); }
 
 ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
   if (!comm || !count) return ncclInvalidArgument;
