@@ -465,9 +465,7 @@ bool aql_usable(pow_ctx* ctx) {
   if (!ctx->aql) return false;
   if (pow_aql_status(ctx->aql) >= 0) return true;
   ctx->aql_why = "the dispatch queue reported an error; back on the HIP launch path";
-#ifdef POW_TEST_HOOKS
   pow_aql_close(ctx->aql);
-#endif
   ctx->aql = nullptr;
   return false;
 }
