@@ -133,7 +133,8 @@ NODE_BIN = os.path.join(PKG, "bin", "pow_node")
 # (-DPOW_NODE_TEST_KNOBS: --hold-first, --idle-below, --private-lead, pauses).
 # The shipped bin/pow_node behaves only as node.cpp does.
 NODE_TEST_BIN = os.path.join(PKG, "bin", "pow_node_test")
-NODE_TEST_KNOBS = ("--pause-ms", "--pause-us", "--winner-pause-us", "--hold-first", "--idle-below", "--private-lead")
+NODE_TEST_KNOBS = ("--pause-ms", "--pause-us", "--winner-pause-us", "--hold-first", "--idle-below", "--private-lead",
+                   "--lead-barrier", "--recv-delay-rank", "--recv-delay-us")
 
 
 def mpi_available() -> bool:

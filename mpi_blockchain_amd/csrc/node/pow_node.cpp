@@ -44,7 +44,8 @@
 // switches the protocol tests need are compiled only into bin/pow_node_test
 // (-DPOW_NODE_TEST_KNOBS, mpi_blockchain_amd/build.py):
 //            [--pause-ms MS | --pause-us US] [--winner-pause-us US] [--hold-first 0|1]
-//            [--idle-below K] [--private-lead K]
+//            [--idle-below K] [--private-lead K [--lead-barrier 0|1]
+//             [--recv-delay-rank R --recv-delay-us US]]
 #include <mpi.h>
 #include <unistd.h>
 
@@ -89,6 +90,9 @@ struct TestKnobs {
                                  // MPI_Barrier, so every rank receives a rival block 1 (a certain fork)
   unsigned idle_below = 0;       // do not mine while the chain is below this index (the blocks
                                  // before it come from other ranks, e.g. the reference's CPU ranks)
+  bool lead_barrier = true;      // --private-lead: the miners' barrier after every migration (0 = round 4's shape)
+  int recv_delay_rank = -1;      // this rank's receive thread sleeps recv_delay_us after the tips'
+  unsigned recv_delay_us = 0;    // barrier, before its first validation (the termination-race reproduction)
   unsigned private_lead = 0;     // K >= 2: every rank mines blocks 1..K on a private branch, then all
                                  // publish their tips after one barrier: each receiver is K behind
                                  // and asks the tip's owner for its chain while that owner asks it
@@ -457,7 +461,7 @@ class Node {
       }
       if (!migrated) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
-    MPI_Barrier(lead_comm_);
+    if (opt_.t.lead_barrier) MPI_Barrier(lead_comm_);
   }
 #endif
 
@@ -631,6 +635,8 @@ int Node::run() {
     if (opt_.t.private_lead >= 2 && !tip_seen_ && st.MPI_TAG == kTagNewBlock && buf.index == opt_.t.private_lead) {
       tip_seen_ = true;
       MPI_Barrier(test_comm_);
+      if (rank_ == opt_.t.recv_delay_rank && opt_.t.recv_delay_us)  // a slow receive thread, on purpose
+        std::this_thread::sleep_for(std::chrono::microseconds(opt_.t.recv_delay_us));
     }
 #endif
     std::lock_guard<std::mutex> g(mu_);
@@ -670,6 +676,9 @@ int main(int argc, char** argv) {
     else if (k == "--hold-first") o.t.hold_first = v != 0;
     else if (k == "--idle-below") o.t.idle_below = (unsigned)std::max(0l, v);
     else if (k == "--private-lead") o.t.private_lead = (unsigned)std::min(5l, std::max(0l, v));  // <= VALIDATION_BLOCKS
+    else if (k == "--lead-barrier") o.t.lead_barrier = v != 0;
+    else if (k == "--recv-delay-rank") o.t.recv_delay_rank = (int)v;
+    else if (k == "--recv-delay-us") o.t.recv_delay_us = (unsigned)std::max(0l, v);
 #endif
     else {
       fprintf(stderr, "pow_node: unknown option %s (race-shaping test knobs are in pow_node_test)\n", k.c_str());

@@ -162,3 +162,45 @@ def test_mutual_chain_request(tmp_path, np_):
     st = [chain_status(c, 10, 9) for c in run.chains.values()]
     assert st and all(ok for ok, _ in st) and any(done for _, done in st), out[-3000:]
     assert_dumps_match_reference(run)
+
+
+def _silent_after_tip(out: str, r: int) -> bool:
+    """Round 4's failure shape: rank r mined its private branch but never
+    logged losing the race (node.cpp:249-253), i.e. never validated a tip."""
+    return len(re.findall(rf"\[{r}\] Bloque privado con index \d ", out)) == 3 and \
+        f"[{r}] Perdí la carrera por varios contra" not in out
+
+
+def test_private_lead_termination_race_reproduced(tmp_path):
+    """Round 4's one failed pass, reproduced on purpose and closed (DESIGN.md
+    §4, "Direct dispatch, round 5").  Rank 3's receive thread is made slow
+    (pow_node_test --recv-delay-rank 3 --recv-delay-us 150000: it sleeps
+    150 ms after the tips' barrier, before its first validation).
+    * Without the miners' barrier after every migration (--lead-barrier 0,
+      round 4's test shape), ranks that migrated mine blocks 4..10 in a few ms
+      and the finisher's MPI_Abort (node.cpp:330) ends the job while rank 3 is
+      still asleep: rc 0, and rank 3 never logs its lost race, the exact shape
+      of the failure, with no GPU launch involved.
+    * With the barrier (the default) the same slow rank holds every miner
+      until it has migrated, and every rank logs its migration."""
+    runs = []
+    for k in range(4):
+        (tmp_path / f"old{k}").mkdir()
+        run = run_network(4, str(tmp_path / f"old{k}"), difficulty=9, blocks=10, timeout=120,
+                          extra_args=("--private-lead", "3", "--lead-barrier", "0",
+                                      "--recv-delay-rank", "3", "--recv-delay-us", "150000"))
+        keep_log(run, f"termination_race_old_shape_{k}")
+        assert run.returncode == 0, run.stdout[-3000:]
+        runs.append(_silent_after_tip(run.stdout, 3))
+    print(f"round-4 shape, slow rank 3: silent in {sum(runs)} of {len(runs)} networks")
+    assert any(runs), "the termination race did not show"
+    for k in range(2):
+        (tmp_path / f"new{k}").mkdir()
+        run = run_network(4, str(tmp_path / f"new{k}"), difficulty=9, blocks=10, timeout=120,
+                          extra_args=("--private-lead", "3", "--recv-delay-rank", "3", "--recv-delay-us", "150000"))
+        keep_log(run, f"termination_race_fixed_{k}")
+        out = run.stdout
+        assert run.returncode == 0, out[-3000:]
+        for r in range(4):
+            assert f"[{r}] Perdí la carrera por varios contra" in out, (r, out[-3000:])
+            assert f"[{r}]: find = 2 | received_blockchain_checks = 1" in out, (r, out[-3000:])

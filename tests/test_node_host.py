@@ -10,7 +10,8 @@ from mpi_blockchain_amd.node import mpi_env
 
 pytestmark = pytest.mark.skipif(not mpi_available(), reason="no MPI in this image")
 
-KNOBS = ("--hold-first", "--idle-below", "--private-lead", "--pause-us", "--pause-ms", "--winner-pause-us")
+KNOBS = ("--hold-first", "--idle-below", "--private-lead", "--pause-us", "--pause-ms", "--winner-pause-us",
+         "--lead-barrier", "--recv-delay-rank", "--recv-delay-us")
 
 
 @pytest.mark.parametrize("knob", KNOBS)
