@@ -541,16 +541,17 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
                     "hashes include the trials peers ran before the winner's hit reached them"}
 
 
-def rank_topology(rank: int, local: int, group) -> dict:
-    """What this rank ran on: its HIP device and the device's PCI address and
-    UUID (torch.cuda.get_device_properties), and RCCL's own view of the
-    group's communicator (pow_group_info: ncclCommCount, ncclCommCuDevice)."""
+def rank_topology(rank: int, local: int, group, miner) -> dict:
+    """What this rank ran on: its HIP device, the device's full PCI address
+    (domain:bus:device.function, pow_device_pci_bus_id: partitions of one GPU
+    differ in the function) and UUID (torch.cuda.get_device_properties), and
+    RCCL's own view of the group's communicator (pow_group_info:
+    ncclCommCount, ncclCommCuDevice)."""
     import torch
 
     p = torch.cuda.get_device_properties(local)
-    out = {"rank": rank, "local_rank": local, "hip_device": local,
-           "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid),
-           "pid": os.getpid(), "host": os.uname().nodename}
+    out = {"rank": rank, "local_rank": local, "hip_device": local, "pci": miner.pci_bus_id().lower(),
+           "uuid": str(p.uuid), "pid": os.getpid(), "host": os.uname().nodename}
     if group is not None:
         try:
             out.update({f"group_{k}": v for k, v in group.info().items()})
@@ -561,13 +562,13 @@ def rank_topology(rank: int, local: int, group) -> dict:
 
 def topology_check(ranks: list[dict], world: int, rccl_library: str | None, transport: str,
                    rehearsal: bool) -> dict:
-    """The N > 1 record's self-check: N distinct GPUs (PCI address and UUID),
-    the group's transport counting N ranks, and each rank's communicator on
-    the rank's own device.  In a rehearsal the ranks share one GPU by design:
+    """The N > 1 record's self-check: N distinct GPUs (full PCI address per
+    host), the group's transport counting N ranks, and each rank's
+    communicator on the rank's own device.  UUIDs are reported (partitions of
+    one GPU may share one).  In a rehearsal the ranks share one GPU by design:
     distinctness is reported, not required."""
     pcis = {(r["host"], r["pci"]) for r in ranks}
-    uuids = {(r["host"], r["uuid"]) for r in ranks}
-    distinct = len(pcis) == world and len(uuids) == world
+    distinct = len(pcis) == world
     counts = [r.get("group_comm_count") for r in ranks]
     count_ok = all(c == world for c in counts)
     dev_ok = all(r.get("group_comm_device") == r["hip_device"] for r in ranks)
@@ -798,10 +799,10 @@ def main():
     # count of ranks (RCCL: ncclCommCount), gathered before anything is timed.
     # At N > 1 a record that cannot show N distinct GPUs under one N-rank
     # communicator is not measured: every rank exits non-zero.
-    topo_ranks = [rank_topology(rank, local, group)]
+    topo_ranks = [rank_topology(rank, local, group, miner)]
     if dist is not None:
         topo_ranks = [None] * world
-        dist.all_gather_object(topo_ranks, rank_topology(rank, local, group))
+        dist.all_gather_object(topo_ranks, rank_topology(rank, local, group, miner))
     rlib = None
     if transport != "gloo":
         try:

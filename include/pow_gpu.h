@@ -108,6 +108,10 @@ enum { POW_LAUNCH_HIP = 0, POW_LAUNCH_DIRECT = 1 };
 int pow_launch_path(const pow_ctx* ctx);
 /* Device properties the roofline uses: CU count and peak engine clock (kHz). */
 int pow_device_info(const pow_ctx* ctx, int* cu_count, int* clock_khz, char* name, size_t name_cap);
+/* The ctx's GPU as "domain:bus:device.function" (hipDeviceGetPCIBusId): the
+ * N > 1 bench's check that its ranks run on N distinct devices (partitions of
+ * one GPU differ in the function). */
+int pow_device_pci_bus_id(const pow_ctx* ctx, char* out, size_t cap);
 
 /* ---- host helpers (no GPU work) ---------------------------------------- */
 /* Counter -> nonce[10] (9 base-62 chars MSB first + NUL).

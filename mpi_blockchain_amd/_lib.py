@@ -102,6 +102,7 @@ def load(test_hooks: bool = False) -> ctypes.CDLL:
         "pow_last_error": ([], ctypes.c_char_p),
         "pow_get_stats": ([ctypes.c_void_p, ctypes.POINTER(PowStats)], ctypes.c_int),
         "pow_launch_path": ([ctypes.c_void_p], ctypes.c_int),
+        "pow_device_pci_bus_id": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
         "pow_device_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                              ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
         "pow_nonce_from_counter": ([ctypes.c_uint64, ctypes.c_char_p], ctypes.c_int),
@@ -156,7 +157,7 @@ def load(test_hooks: bool = False) -> ctypes.CDLL:
 
 
 EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_last_error", "pow_get_stats", "pow_launch_path",
-           "pow_device_info",
+           "pow_device_info", "pow_device_pci_bus_id",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak", "pow_valu_rate", "pow_group_partition", "pow_group_unique_id", "pow_group_init",

@@ -828,6 +828,13 @@ int pow_device_info(const pow_ctx* ctx, int* cu_count, int* clock_khz, char* nam
   return POW_OK;
 }
 
+int pow_device_pci_bus_id(const pow_ctx* ctx, char* out, size_t cap) {
+  if (!ctx || !out || cap < 2) return fail(POW_EINVAL, "null");
+  out[0] = 0;
+  HIP_OK(hipDeviceGetPCIBusId(out, (int)std::min<size_t>(cap, 1024), ctx->device));
+  return POW_OK;
+}
+
 int pow_nonce_from_counter(uint64_t ctr, char nonce[POW_NONCE_SIZE]) {
   if (!nonce) return fail(POW_EINVAL, "null nonce");
   if (ctr >= POW_COUNTER_LIMIT) return fail(POW_EINVAL, "counter >= 62^9");

@@ -80,6 +80,12 @@ class GpuMiner:
         check(self.L.pow_device_info(self.ctx, ctypes.byref(cu), ctypes.byref(clk), name, 256), self.L)
         return {"cu_count": cu.value, "clock_khz": clk.value, "name": name.value.decode()}
 
+    def pci_bus_id(self) -> str:
+        """The GPU as "domain:bus:device.function" (pow_device_pci_bus_id)."""
+        buf = ctypes.create_string_buffer(64)
+        check(self.L.pow_device_pci_bus_id(self.ctx, buf, len(buf)), self.L)
+        return buf.value.decode()
+
     def launch_path(self) -> str:
         """How the latency-bound launches go out (pow_launch_path): "hip"
         (hipLaunchKernel; the shipped library's only path) or "direct" (AQL

@@ -245,10 +245,10 @@ def test_topology_check():
     by PCI address and UUID, the group's transport counting N ranks, each
     communicator on its rank's device.  A rehearsal (ranks sharing one GPU)
     reports non-distinct GPUs without failing; a real run fails on it."""
-    good = [_topo_rank(r, f"0000:{r:02x}:00", f"u{r}", 8, dev=r) for r in range(8)]
+    good = [_topo_rank(r, f"0000:{r:02x}:00.0", f"u{r}", 8, dev=r) for r in range(8)]
     t = bench.topology_check(good, 8, "/x/librccl.so", "rccl", False)
     assert t["ok"] and t["distinct_gpus"] and t["group_comm_count_ok"] and t["group_comm_device_ok"]
-    shared = [_topo_rank(r, "0000:05:00", "u0", 8) for r in range(8)]
+    shared = [_topo_rank(r, "0000:05:00.0", "u0", 8) for r in range(8)]
     assert not bench.topology_check(shared, 8, None, "rccl", False)["ok"]
     t = bench.topology_check(shared, 8, None, "gloo", True)
     assert t["ok"] and not t["distinct_gpus"]
@@ -257,7 +257,10 @@ def test_topology_check():
     wrongdev = [dict(x, group_comm_device=0) for x in good]  # every communicator on GPU 0
     assert not bench.topology_check(wrongdev, 8, None, "rccl", False)["ok"]
     # same PCI address on two hosts is two GPUs
-    two_hosts = [_topo_rank(r, "0000:05:00", "u0", 2, host=f"h{r}") for r in range(2)]
+    two_hosts = [_topo_rank(r, "0000:05:00.0", "u0", 2, host=f"h{r}") for r in range(2)]
     assert bench.topology_check(two_hosts, 2, None, "rccl", False)["distinct_gpus"]
+    # partitions of one GPU (CPX): one bus and device, distinct functions, possibly one UUID
+    cpx = [_topo_rank(r, f"0000:05:00.{r}", "u0", 8, dev=r) for r in range(8)]
+    assert bench.topology_check(cpx, 8, None, "rccl", False)["distinct_gpus"]
     missing = [{k: v for k, v in x.items() if k != "group_comm_count"} for x in good]
     assert not bench.topology_check(missing, 8, None, "rccl", False)["ok"]

@@ -68,8 +68,12 @@ def mminer(request, miner, miner_k1):
 
 
 def test_device_is_gfx950(miner):
+    import re
+
     info = miner.device_info()
     assert info["cu_count"] > 0
+    # the full PCI address the N > 1 bench's topology check compares (function included)
+    assert re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-7]", miner.pci_bus_id().lower()), miner.pci_bus_id()
 
 
 def test_edge_counter_digests(miner, golden, templates):
