@@ -421,8 +421,8 @@ struct ArgPack {
 // (HIP: the stream's status; direct dispatch: the completion signal, the
 // queue's indices and the header in the packet's slot).  The context must not
 // be reused after a watchdog error: its launch may still be queued.
-int wait_published(pow_ctx* ctx, const volatile uint32_t* done, uint32_t seq, const char* what,
-                   uint64_t t0, uint64_t deadline_ns) {
+int wait_published(pow_ctx* ctx, const volatile uint32_t* done, const volatile uint32_t* started, uint32_t seq,
+                   const char* what, uint64_t t0, uint64_t deadline_ns) {
   for (uint32_t n = 1; __atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE) != seq; ++n) {
     if ((n & 0xFFFFu) != 0) continue;
     int st;  // 1 = running, 0 = ended, < 0 = error
@@ -444,8 +444,12 @@ int wait_published(pow_ctx* ctx, const volatile uint32_t* done, uint32_t seq, co
 #ifdef POW_TEST_HOOKS
       if (ctx->aql) path = "launch path direct, " + pow_aql_diag(ctx->aql);
 #endif
-      return fail(POW_EHIP, "%s: watchdog: no result after %.3f s (seq %u, done word %u; %s); the context must not be reused",
-                  what, (mono_ns() - t0) * 1e-9, seq, seen, path.c_str());
+      const uint32_t st_word = __atomic_load_n(const_cast<const uint32_t*>(started), __ATOMIC_ACQUIRE);
+      return fail(POW_EHIP,
+                  "%s: watchdog: no result after %.3f s (seq %u, done word %u; the kernel %s (started word %u); %s); "
+                  "the context must not be reused",
+                  what, (mono_ns() - t0) * 1e-9, seq, seen,
+                  st_word == seq ? "started: its first workgroup ran" : "never started", st_word, path.c_str());
     }
     if (__atomic_load_n(const_cast<const uint32_t*>(done), __ATOMIC_ACQUIRE) == seq) break;
 #ifdef POW_TEST_HOOKS
@@ -548,7 +552,8 @@ int run_search_lat(pow_ctx* ctx, uint64_t start, uint64_t count, unsigned diff, 
   const uint64_t t0 = mono_ns(), deadline = t0 + ctx->watchdog_ns + 2ull * count;
   if (int rc = launch_search_lat(ctx, diff > 32 || ctx->force_full, any, waves_per_simd >= 4, grid, L, deadline))
     return rc;
-  if (int rc = wait_published(ctx, &ctx->h_lat->done, L.seq, "latency kernel", t0, deadline)) return rc;
+  if (int rc = wait_published(ctx, &ctx->h_lat->done, &ctx->h_lat->started, L.seq, "latency kernel", t0, deadline))
+    return rc;
   memcpy(ctx->h_res, (const void*)ctx->h_lat, sizeof(PowResult));
   const double ms = (double)ctx->h_res->ticks / ctx->realtime_khz;
   ctx->stats.kernel_ms += ms;
@@ -691,16 +696,24 @@ int pow_init(int device, pow_ctx** out) {
   chk(hipEventCreate(&ctx->ev0), "hipEventCreate");
   chk(hipEventCreate(&ctx->ev1), "hipEventCreate");
   chk(hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming), "hipEventCreate");
+  // Every copy and fill goes on the context's own stream, never on HIP's null
+  // stream: a process that never touches the null stream holds one hardware
+  // queue per context (HIP creates queues as streams first use them), and the
+  // GPU has 24 compute queue slots for every process on it.  Beyond them the
+  // scheduler time-slices queues and a launch can wait seconds for its queue
+  // to be mapped ("Queue pressure").
   chk(hipMalloc(&ctx->d_blob, sizeof(PowBlob)), "hipMalloc consts/result");
-  if (ctx->d_blob) chk(hipMemset(ctx->d_blob, 0, sizeof(PowBlob)), "hipMemset");
+  if (ctx->d_blob) chk(hipMemsetAsync(ctx->d_blob, 0, sizeof(PowBlob), ctx->stream), "hipMemsetAsync");
   chk(hipMalloc(&ctx->d_lat, sizeof(PowResult)), "hipMalloc latency result");
   chk(hipHostMalloc(&ctx->h_lat, sizeof(PowResult), hipHostMallocMapped | hipHostMallocCoherent),
       "hipHostMalloc latency result");
   if (ctx->d_lat && ctx->h_lat) {
-    PowResult init{};
-    init.min_rel = ~0ull;
-    init.peer_abs = ~0ull;
-    chk(hipMemcpy(ctx->d_lat, &init, sizeof init, hipMemcpyHostToDevice), "hipMemcpy");
+    PowResult* init = ctx->h_lat;  // mapped host memory: the copy's source, read before the stream drains
+    memset(init, 0, sizeof *init);
+    init->min_rel = ~0ull;
+    init->peer_abs = ~0ull;
+    chk(hipMemcpyAsync(ctx->d_lat, init, sizeof *init, hipMemcpyHostToDevice, ctx->stream), "hipMemcpyAsync");
+    if (rc == POW_OK) rc = stream_wait_for(ctx, "pow_init copies", 0);
     chk(hipHostGetDevicePointer((void**)&ctx->d_lat_host, ctx->h_lat, 0), "hipHostGetDevicePointer");
   }
   chk(hipHostMalloc(&ctx->h_one, sizeof(PowHashOut), hipHostMallocMapped | hipHostMallocCoherent),
@@ -891,7 +904,8 @@ int hash_one(pow_ctx* ctx, const pow_block* b, uint8_t* digest, char* hex) {
   const uint32_t seq = ctx->one_seq;
   const uint64_t t0 = mono_ns(), deadline = t0 + ctx->watchdog_ns;
   if (int rc = launch_hash_one(ctx, M, seq, deadline)) return rc;
-  if (int rc = wait_published(ctx, &ctx->h_one->done, seq, "hash kernel", t0, deadline)) return rc;
+  if (int rc = wait_published(ctx, &ctx->h_one->done, &ctx->h_one->started, seq, "hash kernel", t0, deadline))
+    return rc;
   uint32_t dg[8];
   for (int k = 0; k < 8; ++k) dg[k] = __atomic_load_n(&ctx->h_one->digest[k], __ATOMIC_RELAXED);
   ctx->stats = pow_stats{(double)ctx->h_one->ticks / ctx->realtime_khz, 1u, 1u};

@@ -107,6 +107,7 @@ struct DeviceKernels {
   // The device's dispatch queue, shared by every context of the process
   // (created at the first pow_aql_open, destroyed by release_all at exit)
   hsa_queue_t* queue = nullptr;
+  int queue_users = 0;  // open contexts on it: the last to close destroys it (it holds one of the GPU's 24 queue slots)
   std::atomic<int> queue_error{0};
   bool hsa_up = false, reader_up = false, exe_up = false;
   hsa_code_object_reader_t reader{};
@@ -339,30 +340,30 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
   {
     std::lock_guard<std::mutex> g(g_mu);
     dk = device_kernels(device);
-    if (dk->ok && !dk->queue && !(flags & POW_AQL_EXP_OWN_QUEUE) &&
-        hsa_queue_create(dk->agent, kSharedQueueSize, HSA_QUEUE_TYPE_MULTI, on_queue_error, &dk->queue_error,
-                         UINT32_MAX, UINT32_MAX, &dk->queue) != HSA_STATUS_SUCCESS)
-      dk->queue = nullptr;
+    if (dk->ok && !dk->queue && !(flags & POW_AQL_EXP_OWN_QUEUE)) {
+      dk->queue_error.store(0, std::memory_order_relaxed);  // a fresh queue
+      if (hsa_queue_create(dk->agent, kSharedQueueSize, HSA_QUEUE_TYPE_MULTI, on_queue_error, &dk->queue_error,
+                           UINT32_MAX, UINT32_MAX, &dk->queue) != HSA_STATUS_SUCCESS)
+        dk->queue = nullptr;
+    }
     shared = dk->queue;
+    // A queue that has reported an error is dead: new contexts stay on the
+    // HIP launch path (the last context closing destroys it).
+    if (shared && !(flags & POW_AQL_EXP_OWN_QUEUE) && dk->queue_error.load(std::memory_order_acquire)) shared = nullptr;
+    if (shared && !(flags & POW_AQL_EXP_OWN_QUEUE)) ++dk->queue_users;
   }
   if (!dk->ok) {
     if (why) *why = dk->why;
     return -1;
   }
   if (!shared && !(flags & POW_AQL_EXP_OWN_QUEUE)) {
-    if (why) *why = "hsa_queue_create";
-    return -1;
-  }
-  // A queue that has reported an error is dead for the rest of the process:
-  // new contexts stay on the HIP launch path.
-  if (!(flags & POW_AQL_EXP_OWN_QUEUE) && dk->queue_error.load(std::memory_order_acquire)) {
-    if (why) *why = "the device's dispatch queue reported an error earlier in this process";
+    if (why) *why = dk->queue ? "the device's dispatch queue reported an error" : "hsa_queue_create";
     return -1;
   }
   pow_aql* a = new pow_aql;
   a->dk = dk;
   a->flags = flags;
-  a->q = shared;
+  a->q = (flags & POW_AQL_EXP_OWN_QUEUE) ? nullptr : shared;  // (its own queue is made below)
   a->queue_error = &dk->queue_error;
   if (flags & POW_AQL_EXP_STALL_HEADER) {
     const char* e = getenv("POW_AQL_STALL_US");
@@ -424,6 +425,14 @@ void pow_aql_close(pow_aql* a) {
        ++n)
     usleep(1);
   if (a->own_q) hsa_queue_destroy(a->q);
+  if (a->q && !a->own_q) {  // the last context on the shared queue gives its slot back
+    std::lock_guard<std::mutex> g(g_mu);
+    DeviceKernels* dk = const_cast<DeviceKernels*>(a->dk);
+    if (dk->queue == a->q && --dk->queue_users == 0) {
+      hsa_queue_destroy(dk->queue);
+      dk->queue = nullptr;
+    }
+  }
   if (a->signal_up) hsa_signal_destroy(a->done);
   if (a->ring) (void)(a->ring_kind == 1 ? hipHostFree(a->ring) : hipFree(a->ring));
   delete a;

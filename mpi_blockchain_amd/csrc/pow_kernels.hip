@@ -660,8 +660,12 @@ __global__ __launch_bounds__(256) void pow_search_lat(
   // The launch's duration is measured on the GPU (constant-rate realtime
   // counter): the host returns when `done` is published, not at the kernel's
   // completion signal, so it records no HIP events around the launch.
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     __hip_atomic_store(&res->t_start, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // into host memory, not waited for: the host's watchdog tells a launch
+    // that never ran from one that ran and did not finish
+    __hip_atomic_store(&hout->started, L.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   // chunks 1-4's K+W words (PowConsts::kw), one per thread, as in K1
   __shared__ __attribute__((aligned(16))) uint32_t lkw[4 * 64];
   lkw[threadIdx.x] = Cb[threadIdx.x];
@@ -861,6 +865,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void po
     const PowMsg M, PowHashOut* __restrict__ hout, uint32_t seq) {
   (void)M;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0)  // the watchdog's "did it run" word (host memory, not waited for)
+    __hip_atomic_store(&hout->started, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // M is the first kernel argument: read it through the kernarg pointer (its
   // address would make a private copy); uniform indices -> scalar loads.
   const uint32_t* const kw = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();

@@ -150,7 +150,9 @@ struct PowResult {
   unsigned long long t_start;  // K1': s_memrealtime at workgroup 0's start ...
   unsigned long long ticks;    // ... and the last workgroup's exit minus it (published)
   unsigned int done;           // K1': the launch's seq, stored last (system scope): the host
-  unsigned int pad1;           //      polls it instead of waiting for the completion signal
+                               //      polls it instead of waiting for the completion signal
+  unsigned int started;        // K1': the launch's seq, stored by workgroup 0 as it starts (the
+                               //      watchdog's diagnostic: did a stuck launch ever run?)
   PowHit hit[POW_HITS];
 };
 
@@ -169,7 +171,7 @@ struct PowHashOut {
   uint32_t digest[8];
   unsigned long long ticks;
   unsigned int done;
-  unsigned int pad;
+  unsigned int started;  // the launch's seq, stored as the wave starts (the watchdog's diagnostic)
 };
 
 // Constants and result words of a context, contiguous so that one H2D copy

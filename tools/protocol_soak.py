@@ -49,6 +49,7 @@ def main() -> int:
     ap.add_argument("--slow-s", type=float, default=3.0,
                     help="with POW_NODE_LOG_DIR set, keep the output of every run slower than this")
     ap.add_argument("--keep-all", action="store_true", help="with POW_NODE_LOG_DIR set, keep every run's output")
+    ap.add_argument("--keep-going", action="store_true", help="count failed runs instead of stopping at the first")
     a = ap.parse_args()
     extra = ("--hold-first", "1") if a.forced_fork else ("--winner-pause-us", "400", "--pause-us", "200")
     if a.mutual:
@@ -60,7 +61,7 @@ def main() -> int:
         # as the mixed test: GPU set-up before MPI_Init (reference ranks join no
         # start barrier), and blocks 1-3 left to the reference ranks
         extra = ("--serial-init", "1", "--idle-below", "3")
-    walls, forks = [], 0
+    walls, forks, failed = [], 0, 0
     for i in range(a.runs):
         with tempfile.TemporaryDirectory(ignore_cleanup_errors=True) as wd:
             t0 = time.perf_counter()
@@ -103,11 +104,15 @@ def main() -> int:
               flush=True)
         if not ok:
             print(run.stdout[-6000:])
-            return 1
+            failed += 1
+            if not a.keep_going:
+                return 1
     walls.sort()
-    print(f"{a.runs} networks of {a.ranks} GPU + {a.ref} reference ranks at d = {a.difficulty}: all passed; "
-          f"wall median {walls[len(walls) // 2]:.2f} s, max {walls[-1]:.2f} s; {forks} fork-path lines in total")
-    return 0
+    verdict = "all passed" if not failed else f"{failed} FAILED"
+    print(f"{a.runs} networks of {a.ranks} GPU + {a.ref} reference ranks at d = {a.difficulty}: {verdict}; "
+          f"wall median {walls[len(walls) // 2]:.2f} s, max {walls[-1]:.2f} s; "
+          f"{sum(w > a.slow_s for w in walls)} slower than {a.slow_s:g} s; {forks} fork-path lines in total")
+    return 1 if failed else 0
 
 
 if __name__ == "__main__":
