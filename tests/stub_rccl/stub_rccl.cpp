@@ -183,9 +183,13 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
   if (!comm || datatype != ncclUint64 || count > kMaxWords) return ncclInvalidArgument;
   if (op != ncclMin && op != ncclMax && op != ncclSum) return ncclInvalidArgument;
   uint64_t v[kMaxWords] = {0};
-  // The operand was staged on `stream` (pow_group: hipMemcpyAsync H2D): wait for it.
+  // The operand was staged on `stream` (pow_group: hipMemcpyAsync H2D): read it
+  // back on the same stream.  (Never HIP's null stream: that would give every
+  // rank of a rehearsal one hardware queue more, and the GPU has 24 for all of
+  // them; DESIGN.md §7, "Queue pressure".)
+  if (count && hipMemcpyAsync(v, sendbuff, count * 8, hipMemcpyDeviceToHost, stream) != hipSuccess)
+    return ncclUnhandledCudaError;
   if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
-  if (count && hipMemcpy(v, sendbuff, count * 8, hipMemcpyDeviceToHost) != hipSuccess) return ncclUnhandledCudaError;
   Shared* s = comm->sh;
   memcpy(s->slot[comm->rank], v, count * 8);
   if (!barrier(comm)) return ncclSystemError;  // every rank's words are in
