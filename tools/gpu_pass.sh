@@ -12,6 +12,9 @@
 #   fuzz_big         10,000 cases, then 2,000 each on the test library: K1' asm variants
 #                    (POW_LAT_WPS=4), + d > 32 variants, and K1 alone (POW_LAT_MAX=0)
 #   soak_mixed       20 mixed networks: 2 reference ranks + 2 pow_node ranks (tools/protocol_soak.py)
+#   queue_pressure   40 six-rank networks alone, then beside a queue-holding process (tools/queue_pressure.sh)
+#   queue_ab         the null-stream A/B beside the holder, 3 rounds (tools/queue_pressure_ab.sh; build the
+#                    variant first with tools/build_nullstream_variant.sh)
 #   ab_k1 L...       K1 sweep A/B over libpow_gpu.so builds (tools/ab_sweep, 9 alternating windows)
 #   ab_k2 L...       pow_hash_block A/B (tools/ab_k2, 5 x 200 calls)
 #   ttb D L...       time-to-block A/B at difficulty D (tools/ab_ttb, 301 templates)
@@ -22,7 +25,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 S="$R/tools/gpu_step.sh"
 L="$R/mpi_blockchain_amd/libpow_gpu.so"
-STEPS=" tests smoke bench profile fuzz fuzz_big soak_mixed ab_k1 ab_k2 ttb k2_trace pmc_onewave "
+STEPS=" tests smoke bench profile fuzz fuzz_big soak_mixed queue_pressure queue_ab ab_k1 ab_k2 ttb k2_trace pmc_onewave "
 libs() {  # the library arguments of an A/B step
   LIBS=()
   while [ $# -gt 0 ] && [[ "$STEPS" != *" $1 "* ]]; do LIBS+=("$1"); shift; done
@@ -42,6 +45,8 @@ while [ $# -gt 0 ]; do
       POW_LAT_WPS=4 POW_FORCE_FULL=1 $S fuzz_lat_asm_full 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4006 &&
       POW_LAT_MAX=0 $S fuzz_k1only 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4007 || exit $? ;;
     soak_mixed) $S soak_mixed 900 python -u tools/protocol_soak.py --runs 20 --ranks 2 --ref 2 --difficulty 9 || exit $? ;;
+    queue_pressure) bash "$R/tools/queue_pressure.sh" 40 6 || exit $? ;;
+    queue_ab) bash "$R/tools/queue_pressure_ab.sh" 3 || exit $? ;;
     ab_k1) libs "$@"; shift ${#LIBS[@]}; $S ab_k1 400 tools/ab_sweep 9 "${LIBS[@]}" || exit $? ;;
     ab_k2) libs "$@"; shift ${#LIBS[@]}; $S ab_k2 200 tools/ab_k2 5 "${LIBS[@]}" || exit $? ;;
     ttb) d=$1; shift; libs "$@"; shift ${#LIBS[@]}; $S ttb_d$d 300 tools/ab_ttb "$d" 301 "${LIBS[@]}" || exit $? ;;
