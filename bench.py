@@ -33,9 +33,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import statistics
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -43,6 +45,115 @@ sys.path.insert(0, ROOT)
 
 OPS_PER_HASH = 5000  # algorithmic int32 VALU ops per trial
 WINDOW = 1 << 32
+
+
+class RankPhases:
+    """Where this bench rank is, so that no failure of an N-rank job goes
+    unexplained.  The reference's ranks block in MPI_Recv with no bound
+    (node.cpp:155-161); a bench rank that hangs the same way (a peer died
+    before RCCL's communicator formed, a collective a peer never joins) would
+    be killed at the driver's limit with nothing written.  Instead every rank:
+
+    * walks through named phases (import -> process_group -> device_init ->
+      group_init -> topology -> warmup -> steps -> parity -> group_search ->
+      protocol / report), each with a time budget, under one job deadline
+      (BENCH_DEADLINE_S, default 570 s: inside the driver's 600 s limit);
+    * on an exception, a phase or job deadline, or SIGTERM (torch.distributed.run
+      stops the surviving ranks that way once one rank has failed), writes ONE
+      stderr line ``{"bench_rank_failure": {...}}`` — rank, phase, elapsed
+      times, the phases done, the reason — and exits non-zero.
+
+    The deadline and signal checks run on a watcher thread, so they fire while
+    the main thread is blocked inside a C call (pow_group_init, a collective):
+    SIGTERM reaches it through signal.set_wakeup_fd, which the C-level handler
+    writes from whichever thread the signal lands on."""
+
+    DEADLINE_S = 570.0
+
+    def __init__(self, rank: int, world: int, local: int):
+        self.rank, self.world, self.local = rank, world, local
+        self.t0 = time.monotonic()
+        self.phase, self.phase_t0, self.budget = "start", self.t0, None
+        self.done: list = []
+        self.lock = threading.Lock()
+        self.emitted = False
+        self.deadline = self.t0 + float(os.environ.get("BENCH_DEADLINE_S", self.DEADLINE_S))
+        # Tests only: BENCH_TEST_FAIL="<rank>:<phase>" makes that rank raise on
+        # entering that phase (a rank that dies before the group forms).
+        self.inject = os.environ.get("BENCH_TEST_FAIL", "")
+
+    def start(self) -> "RankPhases":
+        if threading.current_thread() is threading.main_thread():
+            r, w = os.pipe()
+            os.set_blocking(w, False)
+            signal.signal(signal.SIGTERM, lambda *_: None)  # acted on by the watcher (wakeup fd)
+            signal.set_wakeup_fd(w, warn_on_full_buffer=False)
+            self._rfd = r
+        else:  # pragma: no cover - bench.main() always runs on the main thread
+            self._rfd = None
+        threading.Thread(target=self._watch, name="bench-phase-watch", daemon=True).start()
+        return self
+
+    def enter(self, name: str, budget_s: float) -> None:
+        with self.lock:
+            now = time.monotonic()
+            self.done.append([self.phase, round(now - self.phase_t0, 3)])
+            self.phase, self.phase_t0, self.budget = name, now, budget_s
+        if self.inject == f"{self.rank}:{name}":
+            raise RuntimeError(f"BENCH_TEST_FAIL: injected failure of rank {self.rank} entering {name}")
+
+    def record(self, reason: str, code: int, **extra) -> dict:
+        now = time.monotonic()
+        return {"bench_rank_failure": dict(
+            rank=self.rank, world=self.world, local_rank=self.local, host=os.uname().nodename, pid=os.getpid(),
+            phase=self.phase, phase_elapsed_s=round(now - self.phase_t0, 3), phase_budget_s=self.budget,
+            elapsed_s=round(now - self.t0, 3), phases_done=self.done[1:], reason=reason, exit_code=code, **extra)}
+
+    def _emit(self, reason: str, code: int, **extra) -> bool:
+        with self.lock:
+            if self.emitted:
+                return False
+            self.emitted = True
+            line = json.dumps(self.record(reason, code, **extra))
+        try:
+            sys.stderr.write(line + "\n")
+            sys.stderr.flush()
+        except Exception:  # pragma: no cover - stderr gone: the exit code still says it
+            pass
+        return True
+
+    def fail(self, code: int, reason: str, **extra) -> None:
+        """A failure the main thread found: the line, then exit `code`."""
+        self._emit(reason, code, **extra)
+        sys.exit(code)
+
+    def abort(self, code: int, reason: str, **extra) -> None:
+        """From the watcher (the main thread may be stuck in C): the line, then
+        _exit without running teardown that could block on a stuck GPU."""
+        if self._emit(reason, code, **extra):
+            os._exit(code)
+
+    def _watch(self) -> None:
+        import select
+
+        while True:
+            if self._rfd is not None:
+                ready, _, _ = select.select([self._rfd], [], [], 0.25)
+                if ready:
+                    sigs = os.read(self._rfd, 64)
+                    if signal.SIGTERM in sigs:
+                        self.abort(128 + signal.SIGTERM, "SIGTERM (the launcher stops the job: another rank failed, "
+                                                         "or the job was cancelled)")
+            else:  # pragma: no cover
+                time.sleep(0.25)
+            now = time.monotonic()
+            with self.lock:
+                over = self.budget is not None and now - self.phase_t0 > self.budget
+                phase, budget = self.phase, self.budget
+            if over:
+                self.abort(7, f"phase '{phase}' ran past its {budget:.0f} s budget (hung?)")
+            if now > self.deadline:
+                self.abort(7, f"job deadline: {self.deadline - self.t0:.0f} s (BENCH_DEADLINE_S) passed")
 
 
 def s0_block():
@@ -410,7 +521,41 @@ def wait_for_exit(pids, timeout: float) -> bool:
 FORK_EVENTS = ("Perdí la carrera", "Conflicto suave", "Conflicto de branch", "TAG_CHAIN_HASH")
 
 
-def protocol_job(world: int, timeout: float = 90) -> dict:
+def node_placement(output: str, world: int, rehearsal: bool) -> dict:
+    """Where the ranks of one `mpiexec -np N pow_node` job mined: the
+    `pow_node device {...}` line each rank writes to stderr at start-up
+    (HIP device, PCI address, host, and which launcher variable chose the
+    device), and the ranks that warned that no node-local rank was set.
+    At N > 1 on real GPUs every rank must sit on its own GPU (distinct host +
+    PCI address); in a rehearsal (ranks sharing one GPU by design) that is
+    reported, not required."""
+    import re
+
+    devs = {}
+    for m in re.finditer(r"^pow_node device (\{.*\})\s*$", output, re.M):
+        try:
+            d = json.loads(m.group(1))
+            devs[d["rank"]] = d
+        except (ValueError, KeyError):
+            continue
+    warned = sorted(int(m.group(1)) for m in re.finditer(r"^pow_node: rank (\d+) of \d+: no node-local rank", output,
+                                                          re.M))
+    ranks = [devs[r] for r in sorted(devs)]
+    distinct = len({(d.get("host"), str(d.get("pci", "")).lower()) for d in ranks}) == world and len(ranks) == world
+    complete = sorted(devs) == list(range(world))
+    ok = complete and not warned and (distinct or rehearsal)
+    out = {"devices": [{k: d.get(k) for k in ("rank", "device", "pci", "host", "local_rank", "local_rank_from")}
+                       for d in ranks],
+           "distinct_gpus": distinct, "all_ranks_reported": complete, "no_local_rank_warnings": warned,
+           "rehearsal": rehearsal, "ok": ok}
+    if not ok:
+        out["failed"] = ("not every rank reported its device" if not complete else
+                         "ranks without a node-local rank (all on GPU 0)" if warned else
+                         f"{world} ranks on fewer than {world} distinct GPUs")
+    return out
+
+
+def protocol_job(world: int, timeout: float = 90, rehearsal: bool = False) -> dict:
     """BASELINE config 5 at the job's size: `mpiexec -np N pow_node`, one MPI
     rank per GPU of this node (pow_node binds node-local rank r to GPU r), the
     reference's protocol (broadcast, validation, chain migration) with GPU
@@ -418,7 +563,10 @@ def protocol_job(world: int, timeout: float = 90) -> dict:
     bench ranks wait idle.  d = 9 (the reference's DEFAULT_DIFFICULTY), d = 25
     (real mining: 10 x 2^25 expected trials) and d = 5 with a forced fork
     (--hold-first: every rank mines its own block 1, published after a
-    barrier, so every rank must resolve rival blocks)."""
+    barrier, so every rank must resolve rival blocks).  Each network's
+    `placement` shows the GPU every rank mined on (node_placement); at N > 1
+    on real GPUs a network whose ranks do not sit on N distinct GPUs is marked
+    failed (`ok` false), as is the whole block."""
     import re
     import tempfile
 
@@ -439,9 +587,17 @@ def protocol_job(world: int, timeout: float = 90) -> dict:
                         "chains_consistent": all(ok for ok, _ in st), "chains_complete": sum(c for _, c in st),
                         "blocks_mined": len(re.findall(r"Agregué un producido", run.stdout)),
                         "fork_events": sum(run.stdout.count(m) for m in FORK_EVENTS),
-                        "hard_errors": run.stdout.count("Error duro")}
+                        "hard_errors": run.stdout.count("Error duro"),
+                        "placement": node_placement(run.stdout, world, rehearsal)}
         except Exception as e:  # pragma: no cover - reported, not fatal
             out[key] = {"error": str(e)[-300:]}
+    nets = [out[k] for k in ("d9", "d25", "d5_forced_fork")]
+    out["distinct_gpus"] = all(n.get("placement", {}).get("distinct_gpus") for n in nets)
+    out["ok"] = all("error" not in n and n["rc"] == 0 and n["placement"]["ok"] for n in nets)
+    if not out["ok"]:
+        out["failed"] = "; ".join(f"{k}: " + (n.get("error") or (f"rc {n['rc']}" if n["rc"] else n["placement"].get(
+            "failed", ""))) for k, n in zip(("d9", "d25", "d5_forced_fork"), nets)
+                                  if "error" in n or n["rc"] or not n["placement"]["ok"])
     return out
 
 
@@ -481,7 +637,39 @@ def ladder(miner, n_templates: int = 101, rungs=(9, 13, 17, 21, 25)) -> dict:
     return out
 
 
-def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 21) -> dict:
+BOARD_STOP_OK_US = 50_000  # a peer that ran out its shard instead (2^32 counters) takes ~470,000 us
+
+
+def board_summary(per_rank: list[dict], stop_us: list[float], world: int) -> dict:
+    """Did the stop board work?  Per rank: the group has the node's board and
+    every search ran bound to it; across ranks: the stop latency of each
+    search with a finder (the last rank's mine return minus the finder's,
+    CLOCK_MONOTONIC on one node).  With a board that is missing or not coherent
+    across GPUs the peers only stop at the round's all-reduce, after their
+    whole shard: the latency is then hundreds of ms, not tens of us."""
+    out = {"per_rank": per_rank,
+           "all_ranks_board": all(r["board_open"] and r["board_bound_every_search"] for r in per_rank),
+           "stop_latency_samples": len(stop_us)}
+    if world == 1:
+        out["stop_latency_us_median"] = None
+        out["peers_stopped_by_board"] = None
+        out["note"] = "one rank: no peers to stop"
+        return out
+    if stop_us:
+        med = statistics.median(stop_us)
+        out["stop_latency_us_median"] = round(med, 1)
+        out["stop_latency_us_max"] = round(max(stop_us), 1)
+        out["peers_stopped_by_board"] = out["all_ranks_board"] and med < BOARD_STOP_OK_US
+    else:
+        out["stop_latency_us_median"] = None
+        out["peers_stopped_by_board"] = None
+    out["note"] = ("stop latency = max over ranks of the time each rank's pow_mine_any returned, minus the "
+                   "finder's (CLOCK_MONOTONIC); peers_stopped_by_board needs every rank bound to the board and a "
+                   f"median under {BOARD_STOP_OK_US} us (a peer that runs out its 2^32-counter shard takes ~470 ms)")
+    return out
+
+
+def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 21, gather=None) -> dict:
     """BASELINE config 4, cooperative form: time-to-block of pow_group_mine_any
     over every GPU of the job (collective; the same templates on every rank).
     Each rank mines its static shard; the first hit stops the node's other
@@ -503,6 +691,8 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
     span = 1 << 48
     rng = random.Random(1)
     times, hashes, counters = [], [], []
+    stop_us, mine_ms, ar_ms, rounds = [], [], [], []
+    bound_every, found = True, 0
     bad = {"no_winner": 0, "nonce": 0, "digest": 0, "solves": 0, "range": 0, "ranks_disagree": 0}
     for _ in range(n_templates):
         b = make_block(rng.randrange(1, 1 << 16), 0, 9, 1700000000 + rng.randrange(256),
@@ -511,6 +701,16 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
         t = time.perf_counter()
         r = group.mine(b, 0, span, d, any_solution=True)
         times.append(time.perf_counter() - t)
+        info = group.last_search()  # this rank's part (pow_group_last_search)
+        bound_every = bound_every and bool(info["board_bound"])
+        found += info["local_found"]
+        mine_ms.append(info["mine_ms"])
+        ar_ms.append(info["allreduce_ms"])
+        rounds.append(info["rounds"])
+        fin = group.allreduce([info["mine_end_ns"] if info["local_found"] else U64MAX], "min")[0]
+        last_end = group.allreduce([info["mine_end_ns"]], "max")[0]
+        if fin != U64MAX and world > 1:
+            stop_us.append((last_end - fin) / 1e3)
         hashes.append(group.allreduce([r.hashes if r else 0], "sum")[0])
         c = r.counter if r else U64MAX
         counters.append(r.counter if r else None)
@@ -528,6 +728,10 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
         for k, x in zip(bad, group.allreduce(v, "max")):
             bad[k] += x
     tot_t = sum(times)
+    mine_info = {"rank": rank, "board_open": bool(info["board_open"]), "board_bound_every_search": bound_every,
+                 "searches_found_here": found, "mine_ms_mean": round(statistics.mean(mine_ms), 3),
+                 "allreduce_ms_mean": round(statistics.mean(ar_ms), 3), "rounds_max": max(rounds)}
+    per_rank = (gather or (lambda o: [o]))(mine_info)
     verified = {"winners_checked": n_templates, "failures": bad, "ok": not any(bad.values()),
                 "how": "nonce == counter's, pow_hash_block(winner) == its block_hash, solves_problem(hash, d), "
                        "0 <= counter < 2^48, all-reduce(min) == all-reduce(max) of the ranks' counters"}
@@ -536,7 +740,7 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
             "time_to_block_ms_mean": round(1e3 * tot_t / n_templates, 3),
             "expected_hashes": 2 ** d, "hashes_all_ranks_mean": int(sum(hashes) / n_templates),
             "hashes_per_s_all_ranks": round(sum(hashes) / tot_t, 1),
-            "counters": counters, "verified": verified,
+            "counters": counters, "verified": verified, "board": board_summary(per_rank, stop_us, world),
             "note": "pow_group_mine_any over all GPUs (static shards, stop board, one all-reduce per round); "
                     "hashes include the trials peers ran before the winner's hit reached them"}
 
@@ -711,6 +915,36 @@ def native_group_error(group, group_err: str | None, world: int, rehearsal: bool
     return None
 
 
+def rank_timing(rank: int, kernel_ms: list, allreduce_ms: list, own_wall_s: float, steps: int) -> dict:
+    """One rank's timed steps: mean HIP-event kernel ms per step, mean wall ms
+    in the step's two all-reduces (pow_group_allreduce_u64; waiting for slower
+    peers included), and the rank's own wall ms per step before the closing
+    barrier."""
+    return {"rank": rank,
+            "kernel_ms": round(statistics.mean(kernel_ms), 3) if kernel_ms else None,
+            "allreduce_ms": round(statistics.mean(allreduce_ms), 3) if allreduce_ms else 0.0,
+            "step_ms": round(1e3 * own_wall_s / max(1, steps), 3)}
+
+
+def timing_block(ranks: list[dict], ms_per_step: float) -> dict:
+    """The N > 1 line's attribution of its step time: per rank kernel,
+    all-reduce and own-step ms, the kernel imbalance (max / min over ranks:
+    one slow GPU shows as > 1), and per rank what is left of the job's step
+    (ms_per_step, the slowest rank's wall) after kernel + all-reduce: host time
+    and waiting at the closing barrier."""
+    ks = [r["kernel_ms"] for r in ranks if r.get("kernel_ms")]
+    return {"per_rank_kernel_ms": [r.get("kernel_ms") for r in ranks],
+            "allreduce_ms_per_step": [r.get("allreduce_ms") for r in ranks],
+            "per_rank_step_ms": [r.get("step_ms") for r in ranks],
+            "per_rank_other_ms": [round(ms_per_step - (r.get("kernel_ms") or 0) - (r.get("allreduce_ms") or 0), 3)
+                                  for r in ranks],
+            "imbalance": round(max(ks) / min(ks), 4) if ks and min(ks) > 0 else None,
+            "slowest_kernel_rank": max(ranks, key=lambda r: r.get("kernel_ms") or 0)["rank"] if ranks else None,
+            "note": "kernel = HIP-event time of the step's sweep; allreduce = wall time of its two "
+                    "pow_group_allreduce_u64 calls (min, sum), waiting for peers included; other = ms_per_step "
+                    "minus both"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -735,28 +969,50 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ph = RankPhases(rank, world, local).start()
+    try:
+        run_rank(args, ph, world, rank, local)
+    except SystemExit:
+        raise
+    except BaseException as e:  # every rank's failure leaves its line: which phase, why
+        import traceback
+
+        ph.fail(6, f"exception: {type(e).__name__}: {str(e)[-400:]}",
+                traceback=traceback.format_exc(limit=6)[-1500:])
+
+
+def run_rank(args, ph: RankPhases, world: int, rank: int, local: int) -> None:
+    """One bench rank, phase by phase (RankPhases)."""
+    ph.enter("import", 240)  # the first `import torch` on a fresh box pages the image in (1-2 min)
     import torch
 
     dist = None
+    rehearsal = os.environ.get("BENCH_REHEARSAL") == "1"
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or os.environ.get("BENCH_FORCE_DIST") == "1":
+        import datetime
+
         import torch.distributed as dist
 
+        # A peer that never joins fails the rendezvous and torch's collectives
+        # in 120 s, inside the driver's 600 s limit (torch's default is ~10 min).
+        ph.enter("process_group", 150)
+        pg_timeout = datetime.timedelta(seconds=120)
         # BENCH_REHEARSAL=1 (tests only): several ranks share the visible
         # GPU(s) and talk over gloo, to exercise the N > 1 path on a one-GPU
         # box (RCCL refuses two ranks on one device).  The numbers it prints
         # are not a scaling measurement.
-        if os.environ.get("BENCH_REHEARSAL") == "1":
-            local = local % torch.cuda.device_count()
+        if rehearsal:
+            dist.init_process_group("gloo", timeout=pg_timeout)
+            local = local % max(1, torch.cuda.device_count())
             torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
 
+    ph.enter("device_init", 120)
     from mpi_blockchain_amd.miner import DeviceBuffer, GpuMiner
     from mpi_blockchain_amd.shard import RcclGroup, ShardedMiner, rccl_path
 
-    rehearsal = os.environ.get("BENCH_REHEARSAL") == "1"
     # A rehearsal (ranks sharing one GPU; tests only) runs the same pow_group
     # rounds with the all-reduce either over gloo (pow_group_init_custom;
     # BENCH_REHEARSAL_TRANSPORT=gloo, the default) or through pow_group_init's
@@ -770,6 +1026,9 @@ def main():
     miner = GpuMiner(local, test_hooks=transport == "rccl_stub")
     # The library's own RCCL communicator (the id travels over torch.distributed);
     # at N = 1 a one-rank group, used only by the group_search measurement.
+    # pow_group_init gives up after 60 s if a peer never joins (non-blocking
+    # ncclCommInitRankConfig under a deadline).
+    ph.enter("group_init", 120)
     group, group_err = None, None
     if transport == "gloo":
         group = ShardedMiner(miner, rank, world)
@@ -783,7 +1042,8 @@ def main():
         if dist is not None:
             # Every rank uses the native group or none does (a rank that lacks it
             # would leave its peers waiting in the group's collectives).
-            ok = torch.tensor([1 if group is not None else 0], dtype=torch.int64, device=f"cuda:{local}")
+            ok = torch.tensor([1 if group is not None else 0], dtype=torch.int64,
+                              device="cpu" if rehearsal else f"cuda:{local}")
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             if int(ok.item()) == 0 and group is not None:
                 group.close()
@@ -791,14 +1051,12 @@ def main():
                 group_err = "pow_group_init failed on a peer rank"
         err = native_group_error(group, group_err, world, transport == "gloo")
         if err:  # fail loudly: no N > 1 number without the native collectives
-            print(json.dumps({"error": "bench.py: no native pow_group at N > 1", "group_error": err, "rank": rank}),
-                  file=sys.stderr, flush=True)
-            dist.destroy_process_group()
-            sys.exit(3)
+            ph.fail(3, "bench.py: no native pow_group at N > 1", group_error=err)
     # Who took part: every rank's GPU (PCI address, UUID) and the group's own
     # count of ranks (RCCL: ncclCommCount), gathered before anything is timed.
     # At N > 1 a record that cannot show N distinct GPUs under one N-rank
     # communicator is not measured: every rank exits non-zero.
+    ph.enter("topology", 60)
     topo_ranks = [rank_topology(rank, local, group, miner)]
     if dist is not None:
         topo_ranks = [None] * world
@@ -811,10 +1069,7 @@ def main():
             rlib = f"unknown ({e})"
     topology = topology_check(topo_ranks, world, rlib, transport, rehearsal)
     if world > 1 and not topology["ok"]:
-        print(json.dumps({"error": "bench.py: topology check failed at N > 1", "topology": topology, "rank": rank}),
-              file=sys.stderr, flush=True)
-        dist.destroy_process_group()
-        sys.exit(4)
+        ph.fail(4, "bench.py: topology check failed at N > 1", topology=topology)
     info = miner.device_info()
     tmpl = s0_block()
     d = args.difficulty
@@ -822,9 +1077,9 @@ def main():
     cap = 12_000_000  # > 2^32 / 2^9 * 1.4
     buf = DeviceBuffer(miner, 4 * cap)
     if dist is not None and group is None:
-        red = torch.zeros(2, dtype=torch.int64, device=f"cuda:{local}")
+        red = torch.zeros(2, dtype=torch.int64, device="cpu" if rehearsal else f"cuda:{local}")
 
-    kernel_ms = []
+    kernel_ms, allreduce_ms = [], []
 
     local_last = [None]  # this rank's (solutions, lowest counter) of the last step
 
@@ -833,17 +1088,23 @@ def main():
         kernel_ms.append(miner.stats()["kernel_ms"])
         local_last[0] = (n, mn)
         if dist is not None and group is not None:  # RCCL through pow_group_allreduce_u64
+            a0 = time.perf_counter()
             lo = group.allreduce([mn if mn is not None else (1 << 64) - 1], "min")[0]
             tot = group.allreduce([n], "sum")[0]
+            allreduce_ms.append(1e3 * (time.perf_counter() - a0))
             return tot, lo
         if dist is not None:  # rehearsal (several ranks share one GPU over gloo), or no native group
+            a0 = time.perf_counter()
             red[0] = mn if mn is not None else (1 << 63) - 1
             dist.all_reduce(red[0:1], op=dist.ReduceOp.MIN)
             red[1] = n
             dist.all_reduce(red[1:2], op=dist.ReduceOp.SUM)
-            return int(red[1].item()), int(red[0].item())
+            out = int(red[1].item()), int(red[0].item())
+            allreduce_ms.append(1e3 * (time.perf_counter() - a0))
+            return out
         return n, mn
 
+    ph.enter("warmup", 60 + 30 * args.warmup)
     first = None
     for _ in range(args.warmup):
         first = step()
@@ -851,40 +1112,56 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     kernel_ms.clear()
+    allreduce_ms.clear()
+    ph.enter("steps", 60 + 30 * args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
     torch.cuda.synchronize()
+    el_own = time.perf_counter() - t0  # this rank's own steps, before it waits for the others
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([el], dtype=torch.float64, device="cpu" if rehearsal else f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
     # Per-rank parity (outside the timed region): every rank's window whose
     # fingerprints are committed (rank 0: [0, 2^32); rank 7: [7*2^32, 8*2^32),
-    # the farthest window of an 8-GPU run) is checked against them.
+    # the farthest window of an 8-GPU run) is checked against them.  With it,
+    # each rank's own timing: its mean kernel ms and all-reduce ms per step and
+    # its own steps' wall (a sub-linear N > 1 result is attributable from the
+    # record: one slow GPU, the collective, or host time between them).
+    ph.enter("parity", 120)
     n_loc = local_last[0][0]
     local_last[0] = (*local_last[0], list_fingerprint(buf, n_loc) if d == 9 and n_loc <= cap else None)
-    per_rank = [local_last[0]]
+    my_timing = rank_timing(rank, kernel_ms, allreduce_ms, el_own, args.steps)
+    per_rank = [(local_last[0], my_timing)]
     if dist is not None:
         per_rank = [None] * world
-        dist.all_gather_object(per_rank, local_last[0])
+        dist.all_gather_object(per_rank, (local_last[0], my_timing))
+    timing = timing_block([t for _, t in per_rank], 1e3 * el / args.steps)
+    per_rank = [p for p, _ in per_rank]
     gsearch = None
     if group is not None and not args.no_group_search:
+        ph.enter("group_search", 300)
+
+        def gather(obj):
+            if dist is None:
+                return [obj]
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+
         try:
-            gsearch = group_search(group, rank, world)
+            gsearch = group_search(group, rank, world, gather=gather)
         except Exception as e:  # pragma: no cover - reported, not fatal: the headline is measured
             gsearch = {"error": str(e)[-300:]}
         # A winner that does not verify (identical verdict on every rank: all-reduced)
         # makes an N > 1 record unusable: exit non-zero like a missing group.
         if world > 1 and "verified" in gsearch and not gsearch["verified"]["ok"]:
-            print(json.dumps({"error": "bench.py: group_search winners failed verification",
-                              "verified": gsearch["verified"], "rank": rank}), file=sys.stderr, flush=True)
-            dist.destroy_process_group()
-            sys.exit(5)
+            ph.fail(5, "bench.py: group_search winners failed verification", verified=gsearch["verified"])
     # Config 5 on this job's GPUs: rank 0 launches the MPI job once every
     # other bench rank has exited (their processes release the GPUs, so each
     # GPU carries one pow_node rank and at most bench rank 0 besides).
@@ -895,14 +1172,19 @@ def main():
         pids = [None] * world
         dist.all_gather_object(pids, os.getpid())
     if rank != 0:
+        ph.enter("teardown", 60)
         buf.free()
         if group is not None:
             group.close()
         dist.destroy_process_group()
         return
     if do_proto:
+        ph.enter("protocol_wait", 150)
         gone = wait_for_exit(pids[1:], timeout=120)
-        proto = protocol_job(world) if gone else {"skipped": "bench ranks 1..N-1 did not exit within 120 s"}
+        ph.enter("protocol", 360)
+        proto = protocol_job(world, rehearsal=rehearsal) if gone else \
+            {"skipped": "bench ranks 1..N-1 did not exit within 120 s"}
+    ph.enter("report", 480)
     collective = ("gloo all_reduce(min,sum) per step via pow_group_allreduce_u64 (pow_group_init_custom; "
                   "rehearsal: ranks share one GPU)" if transport == "gloo" and rehearsal and group is not None else
                   "stand-in RCCL (tests/stub_rccl, shared memory) all_reduce(min,sum) per step via "
@@ -976,6 +1258,8 @@ def main():
                    "parallelism": f"static nonce shards x{world}; collective: {collective}"},
         "hashes_per_s_per_gpu": round(value / world, 1),
         "kernel_ms_per_step": round(kms, 3),
+        "timing": timing,
+        "imbalance": timing["imbalance"],
         "roofline": roofline_block(achieved, kms, peak, live, traffic, traffic_source, 4 * (last[0] or 0),
                                    info["cu_count"]),
         "device": info,
@@ -995,10 +1279,11 @@ def main():
         res["protocol"]["validation_hash"] = validation_latency()
     if proto is not None:
         res["protocol"] = proto
+    print(json.dumps(res), flush=True)
+    ph.enter("teardown", 60)
     buf.free()
     if group is not None:
         group.close()
-    print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

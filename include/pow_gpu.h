@@ -265,7 +265,13 @@ void pow_group_partition(uint64_t start, uint64_t count, int rank, int nranks,
 /* Rank 0 makes the id; the caller hands it to every rank (MPI_Bcast, a file,
  * torch.distributed ...) before pow_group_init. */
 int pow_group_unique_id(uint8_t id[POW_GROUP_ID_BYTES]);
-/* Joins the RCCL communicator on ctx's GPU; returns once all ranks joined. */
+/* Joins the RCCL communicator on ctx's GPU; returns once all ranks joined.
+ * Bounded: the communicator is made non-blocking (ncclCommInitRankConfig,
+ * config.blocking = 0) and polled (ncclCommGetAsyncError) until every rank
+ * joined or 60 s (POW_GROUP_INIT_TIMEOUT_MS) passed; then it is aborted
+ * (ncclCommAbort) and POW_ECOMM names the rank, nranks, device and elapsed
+ * time.  (The reference's ranks block in MPI_Recv with no bound,
+ * node.cpp:155-161.) */
 int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
                    pow_group** out);
 /* The same group over a reduction the caller supplies instead of RCCL: the
@@ -300,8 +306,24 @@ int pow_group_info(const pow_group* g, int* comm_count, int* comm_device);
  * librccl.so.1 from the library search path.  POW_ECOMM if RCCL cannot be
  * loaded. */
 int pow_group_rccl_path(char* path, size_t cap);
-/* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream. */
+/* In-place all-reduce of n <= 8 uint64 words (POW_REDUCE_*), on ctx's stream.
+ * A collective that fails or passes its deadline leaves the group broken:
+ * every later collective of it returns POW_ECOMM at once (destroy it). */
 int pow_group_allreduce_u64(pow_group* g, uint64_t* vals, size_t n, int op);
+/* What this rank did in the group's last pow_group_mine[_any] call (no GPU
+ * work, no collective): the N > 1 bench's record of whether the stop board
+ * worked (a missing board shows as peers that run out their shards: a large
+ * spread between the finder's and the last peer's mine_end_ns). */
+typedef struct pow_group_search_info {
+  int board_open;        /* the group has the node's stop board (pow_group_init opened it) */
+  int board_bound;       /* the last search ran with this rank's context bound to it */
+  uint32_t rounds;       /* rounds of the last search (one all-reduce each) */
+  int local_found;       /* this rank's own launch found a solution in the last round */
+  uint64_t mine_end_ns;  /* CLOCK_MONOTONIC when that launch returned (0: none ran) */
+  double mine_ms;        /* wall ms in this rank's own launches, all rounds */
+  double allreduce_ms;   /* wall ms in the rounds' all-reduces, waiting for peers included */
+} pow_group_search_info;
+int pow_group_last_search(const pow_group* g, pow_group_search_info* out);
 /* On one node the ranks also share a stop board (named after the id, opened
  * by pow_group_init): a rank's hit stops the other GPUs inside their running
  * launches, not only at the round's all-reduce.

@@ -65,6 +65,15 @@ class ValuResult(ctypes.Structure):
                 ("clock_hz", ctypes.c_double), ("cycles_per_instr", ctypes.c_double)]
 
 
+class GroupSearchInfo(ctypes.Structure):
+    """pow_group_search_info (include/pow_gpu.h): this rank's part in the
+    group's last search."""
+
+    _fields_ = [("board_open", ctypes.c_int), ("board_bound", ctypes.c_int), ("rounds", ctypes.c_uint32),
+                ("local_found", ctypes.c_int), ("mine_end_ns", ctypes.c_uint64), ("mine_ms", ctypes.c_double),
+                ("allreduce_ms", ctypes.c_double)]
+
+
 POW_VALU_MIX, POW_VALU_FULL, POW_VALU_HALF = 0, 1, 2
 POW_LAUNCH_HIP, POW_LAUNCH_DIRECT = 0, 1
 
@@ -133,6 +142,7 @@ def load(test_hooks: bool = False) -> ctypes.CDLL:
         "pow_group_destroy": ([ctypes.c_void_p], None),
         "pow_group_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "pow_group_rccl_path": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        "pow_group_last_search": ([ctypes.c_void_p, ctypes.POINTER(GroupSearchInfo)], ctypes.c_int),
         "pow_group_allreduce_u64": ([ctypes.c_void_p, c_u64p, ctypes.c_size_t, ctypes.c_int], ctypes.c_int),
         "pow_group_mine": ([ctypes.c_void_p, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
                             ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, P, c_u64p, c_u64p], ctypes.c_int),
@@ -161,7 +171,8 @@ EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_las
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak", "pow_valu_rate", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
-           "pow_group_init_custom", "pow_group_destroy", "pow_group_info", "pow_group_rccl_path", "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",
+           "pow_group_init_custom", "pow_group_destroy", "pow_group_info", "pow_group_rccl_path", "pow_group_last_search",
+           "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",
            "pow_board_open", "pow_board_unlink", "pow_board_close", "pow_board_bind", "pow_board_post",
            "pow_board_peek")
 

@@ -140,6 +140,7 @@ class Node {
   Node(const Options& o) : opt_(o) {}
 
   int init_gpu();
+  void report_device();
   int run();
 #ifdef POW_NODE_TEST_KNOBS
   // --log-chain-stdin <rank> (test build): no MPI, no GPU.  Load a chain from
@@ -184,6 +185,8 @@ class Node {
   MPI_Datatype block_type_{};
   pow_ctx* mine_ctx_ = nullptr;              // used only by the mining thread
   pow_ctx* recv_ctx_ = nullptr;              // used only by the receive thread
+  int device_ = -1, visible_gpus_ = 0, local_rank_ = 0;
+  const char* local_rank_from_ = nullptr;    // the launcher variable the device came from (null: none)
   std::deque<std::pair<pow_block, MPI_Status>> deferred_;
 #ifdef POW_NODE_TEST_KNOBS
   std::atomic<int> rivals1_{0};  // --hold-first: peers' blocks 1 this rank has processed
@@ -568,7 +571,8 @@ class Node {
 // has passed the start barrier in main().  (--serial-init 1
 // runs it before MPI_Init instead: then no reference rank of a mixed job can
 // start mining while a GPU rank is still initialising.)  The device is the
-// node-local rank (from the launcher's environment) modulo the visible GPUs.
+// node-local rank (from the launcher's environment) modulo the visible GPUs;
+// report_device says which one it was and where the choice came from.
 int Node::init_gpu() {
   int ndev = 0, local = 0;
   if (pow_device_count(&ndev) != POW_OK || ndev < 1) {
@@ -576,14 +580,50 @@ int Node::init_gpu() {
     return 1;
   }
   for (const char* k : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "PMI_RANK"})
-    if (const char* e = getenv(k)) { local = atoi(e); break; }
+    if (const char* e = getenv(k)) {
+      local = atoi(e);
+      local_rank_from_ = k;
+      break;
+    }
   const int dev = opt_.device >= 0 ? opt_.device : local % ndev;
+  device_ = dev;
+  visible_gpus_ = ndev;
+  local_rank_ = local;
   if (pow_init(dev, &mine_ctx_) != POW_OK || pow_init(dev, &recv_ctx_) != POW_OK ||
       pow_warmup(mine_ctx_) != POW_OK || pow_warmup(recv_ctx_) != POW_OK) {
     fprintf(stderr, "pow_init(%d): %s\n", dev, pow_last_error());
     return 1;
   }
   return 0;
+}
+
+// One stderr line per rank at start-up, after MPI_Init: the GPU this rank
+// mines on (HIP index and PCI address) and where the choice came from, so a
+// job's placement can be checked (bench.py's config-5 block requires one rank
+// per distinct GPU at N > 1).  The reference runs one process per node
+// (node.cpp:379-396) and has no device to choose.  A job of several ranks
+// whose launcher set no node-local rank would put every rank on GPU 0: that
+// is said on stderr rather than done silently.
+void Node::report_device() {
+  int rank = 0, size = 1;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  char pci[64] = "?";
+  if (pow_device_pci_bus_id(mine_ctx_, pci, sizeof pci) != POW_OK) snprintf(pci, sizeof pci, "?");
+  char host[128] = "?";
+  if (gethostname(host, sizeof host) != 0) snprintf(host, sizeof host, "?");
+  host[sizeof host - 1] = 0;
+  const char* from = opt_.device >= 0 ? "--device" : local_rank_from_ ? local_rank_from_ : "none";
+  fprintf(stderr,
+          "pow_node device {\"rank\": %d, \"size\": %d, \"device\": %d, \"pci\": \"%s\", \"host\": \"%s\", "
+          "\"pid\": %d, \"local_rank\": %d, \"local_rank_from\": \"%s\", \"visible_gpus\": %d}\n",
+          rank, size, device_, pci, host, (int)getpid(), local_rank_, from, visible_gpus_);
+  if (opt_.device < 0 && !local_rank_from_ && size > 1)
+    fprintf(stderr,
+            "pow_node: rank %d of %d: no node-local rank in the environment (MPI_LOCALRANKID, "
+            "OMPI_COMM_WORLD_LOCAL_RANK, LOCAL_RANK, PMI_RANK): mining on GPU %d like every other such rank; "
+            "launch with mpiexec or pass --device\n",
+            rank, size, device_);
 }
 
 int Node::run() {
@@ -720,6 +760,7 @@ int main(int argc, char** argv) {
   // One start line for every rank (see the header): GPU set-up ended at a
   // different time on each rank.  With --serial-init, MPI_Init was it.
   if (!o.serial_init) MPI_Barrier(MPI_COMM_WORLD);
+  n.report_device();
 #ifdef POW_NODE_TEST_KNOBS
   // Start-up split (test build only, stderr): where a slow network's first
   // second goes (GPU set-up: HIP runtime + two contexts + warm-up; MPI_Init).

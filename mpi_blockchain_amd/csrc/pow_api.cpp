@@ -241,6 +241,11 @@ struct pow_ctx {
   // Watchdog (every host wait on a launch is bounded): base deadline of a
   // latency launch, and of a throughput launch on top of its per-counter share.
   uint64_t watchdog_ns = 10ull * 1000000000ull;
+  // A watchdog fired (or a direct dispatch was refused after its packet slot
+  // was reserved): a launch of this context may still be queued and write its
+  // buffers, whatever the launch path.  pow_destroy then leaks them, and
+  // pow_group_* do not queue a collective behind the stuck launch.
+  bool wedged = false;
   pow_stats stats{};
 };
 
@@ -303,10 +308,12 @@ int stream_wait(pow_ctx* ctx, const char* what, uint64_t t0, uint64_t deadline_n
     }
   }
   if (slack > 1000) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
-  if (late)
+  if (late) {
+    ctx->wedged = true;
     return fail(POW_EHIP, "%s: watchdog: not complete after %.3f s (deadline %.3f s; hipStreamQuery: %s); "
                 "the context must not be reused",
                 what, (mono_ns() - t0) * 1e-9, (deadline_ns - t0) * 1e-9, hipGetErrorString(hipStreamQuery(ctx->stream)));
+  }
   HIP_OK(q);
   HIP_OK(hipStreamSynchronize(ctx->stream));
   return POW_OK;
@@ -445,6 +452,7 @@ int wait_published(pow_ctx* ctx, const volatile uint32_t* done, const volatile u
       if (ctx->aql) path = "launch path direct, " + pow_aql_diag(ctx->aql);
 #endif
       const uint32_t st_word = __atomic_load_n(const_cast<const uint32_t*>(started), __ATOMIC_ACQUIRE);
+      ctx->wedged = true;
       return fail(POW_EHIP,
                   "%s: watchdog: no result after %.3f s (seq %u, done word %u; the kernel %s (started word %u); %s); "
                   "the context must not be reused",
@@ -469,7 +477,7 @@ bool aql_usable(pow_ctx* ctx) {
   if (!ctx->aql) return false;
   if (pow_aql_status(ctx->aql) >= 0) return true;
   ctx->aql_why = "the dispatch queue reported an error; back on the HIP launch path";
-  pow_aql_close(ctx->aql);
+  if (!pow_aql_close(ctx->aql)) ctx->wedged = true;  // a packet may still be in flight
   ctx->aql = nullptr;
   return false;
 }
@@ -483,8 +491,10 @@ int launch_hash_one(pow_ctx* ctx, const PowMsg& M, uint32_t seq, uint64_t deadli
     a.put(ctx->d_one);
     a.put(seq);
     std::string why;
-    if (pow_aql_dispatch(ctx->aql, POW_AQL_HASH_ONE, 1, 64, a.b, a.n, deadline_ns, &why))
+    if (pow_aql_dispatch(ctx->aql, POW_AQL_HASH_ONE, 1, 64, a.b, a.n, deadline_ns, &why)) {
+      ctx->wedged = true;  // a refused packet may have left its reserved slot behind (pow_aql_dispatch)
       return fail(POW_EHIP, "dispatch of pow_hash_one failed: %s (%s)", why.c_str(), pow_aql_diag(ctx->aql).c_str());
+    }
     return POW_OK;
   }
 #endif
@@ -507,8 +517,10 @@ int launch_search_lat(pow_ctx* ctx, bool full, bool any, bool asm_groups, unsign
     a.put(ctx->d_lat_host);
     const int k = POW_AQL_LAT0 + (full ? 1 : 0) + (any ? 2 : 0) + (asm_groups ? 4 : 0);
     std::string why;
-    if (pow_aql_dispatch(ctx->aql, k, grid, 256, a.b, a.n, deadline_ns, &why))
+    if (pow_aql_dispatch(ctx->aql, k, grid, 256, a.b, a.n, deadline_ns, &why)) {
+      ctx->wedged = true;
       return fail(POW_EHIP, "dispatch of pow_search_lat failed: %s (%s)", why.c_str(), pow_aql_diag(ctx->aql).c_str());
+    }
     return POW_OK;
   }
 #endif
@@ -624,6 +636,7 @@ bool cancel_moved(const volatile uint32_t* cancel_word, uint32_t epoch) {
 }
 
 int pow_ctx_device(const pow_ctx* ctx) { return ctx->device; }
+bool pow_ctx_wedged(const pow_ctx* ctx) { return ctx->wedged; }
 void pow_ctx_set_stats(pow_ctx* ctx, const pow_stats& s) { ctx->stats = s; }
 void* pow_ctx_stream(const pow_ctx* ctx) { return (void*)ctx->stream; }
 int pow_ctx_stream_wait(pow_ctx* ctx, const char* what, uint64_t budget_ns) {
@@ -750,13 +763,16 @@ int pow_init(int device, pow_ctx** out) {
 void pow_destroy(pow_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  // Bounded too (the base deadline + 10 s): a context whose launch never
-  // completed (a watchdog error) is left allocated rather than freed under a
-  // kernel that may still write it.  (No event: pow_init failed before any
-  // launch, nothing is queued.)
+  // A context whose launch never completed (a watchdog error, on either launch
+  // path: direct-dispatch packets are not on the stream, so a stream wait
+  // would not see them) is left allocated rather than freed under a kernel
+  // that may still write it.  Otherwise the wait is bounded too (the base
+  // deadline + 10 s).  (No event: pow_init failed before any launch, nothing
+  // is queued.)
+  if (ctx->wedged) return;
   if (ctx->stream && ctx->ev_block && stream_wait_for(ctx, "pow_destroy", 10ull * 1000000000ull) != POW_OK) return;
 #ifdef POW_TEST_HOOKS
-  pow_aql_close(ctx->aql);
+  if (!pow_aql_close(ctx->aql)) return;  // its last packet did not complete: keep what it may write
 #endif
   (void)hipFree(ctx->d_blob);
   if (ctx->h_blob) (void)hipHostFree(ctx->h_blob);

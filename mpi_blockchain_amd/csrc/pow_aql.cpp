@@ -312,6 +312,10 @@ struct pow_aql {
 };
 
 namespace {
+// The value the host stores into a queue's error word when it abandons a
+// reserved packet slot (not an HSA status): the queue is dead from then on.
+constexpr int kQueueDead = 0x7D0D;
+
 void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
   static_cast<std::atomic<int>*>(data)->store((int)st, std::memory_order_release);
 }
@@ -415,15 +419,20 @@ int pow_aql_open(int device, unsigned flags, pow_aql** out, std::string* why) {
   return 0;
 }
 
-void pow_aql_close(pow_aql* a) {
-  if (!a) return;
+bool pow_aql_close(pow_aql* a) {
+  if (!a) return true;
   // Launches are host-waited, so none of this context's is in flight unless
   // one failed mid-flight: wait (bounded, ~1 s) for the last one to complete
   // before its argument ring and signal go.
-  for (int n = 0; n < 1000000 && a->signal_up && a->q && hsa_signal_load_scacquire(a->done) != 0 &&
+  const bool sig = a->signal_up && a->q && !(a->flags & POW_AQL_EXP_NO_SIGNAL);
+  for (int n = 0; n < 1000000 && sig && hsa_signal_load_scacquire(a->done) != 0 &&
                   !a->queue_error->load(std::memory_order_acquire);
        ++n)
     usleep(1);
+  // Still counted in flight (the wait ran out, or the queue died under it):
+  // the packet may still run, so its argument slot, its signal, the queue and
+  // the caller's buffers stay as they are (leaked, not freed under it).
+  if (sig && hsa_signal_load_scacquire(a->done) != 0) return false;
   if (a->own_q) hsa_queue_destroy(a->q);
   if (a->q && !a->own_q) {  // the last context on the shared queue gives its slot back
     std::lock_guard<std::mutex> g(g_mu);
@@ -436,6 +445,7 @@ void pow_aql_close(pow_aql* a) {
   if (a->signal_up) hsa_signal_destroy(a->done);
   if (a->ring) (void)(a->ring_kind == 1 ? hipHostFree(a->ring) : hipFree(a->ring));
   delete a;
+  return true;
 }
 
 int pow_aql_status(const pow_aql* a) {
@@ -500,11 +510,23 @@ int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_si
   // consuming this queue: the reserved slot is left INVALID (nothing may be
   // written into a slot the processor has not released), and the caller gets
   // the error and the diagnostic.
+  // Either way the queue is then marked dead (kQueueDead): the packet
+  // processor stops at the INVALID slot, so every later packet of every
+  // context on the queue would stall; aql_usable sends them all back to the
+  // HIP launch path instead.
   const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
   a->last_idx = idx;
   for (uint32_t n = 0; idx - hsa_queue_load_read_index_scacquire(q) >= q->size; ++n) {
-    if (a->queue_error->load(std::memory_order_acquire)) return refuse("the queue reported an error");
-    if ((n & 1023u) == 1023u && now_ns() > deadline_ns) return refuse("no free packet slot before the deadline");
+    if (a->queue_error->load(std::memory_order_acquire)) {
+      int zero = 0;
+      a->queue_error->compare_exchange_strong(zero, kQueueDead, std::memory_order_acq_rel);
+      return refuse("the queue reported an error");
+    }
+    if ((n & 1023u) == 1023u && now_ns() > deadline_ns) {
+      int zero = 0;
+      a->queue_error->compare_exchange_strong(zero, kQueueDead, std::memory_order_acq_rel);
+      return refuse("no free packet slot before the deadline; the queue is marked dead");
+    }
   }
   // in flight += 1; the packet processor subtracts 1 when the launch
   // completes (which may be after the caller has seen the kernel's done word

@@ -37,14 +37,23 @@ enum {
   // later packet (and doorbell) overtakes it (tests/test_gpu_parity.py).
   POW_AQL_EXP_STALL_HEADER = 512,
 };
-void pow_aql_close(pow_aql* a);
+// Closes the dispatcher once its last packet has completed (a bounded wait,
+// ~1 s).  true = closed (null is); false = the wait ran out or the queue is
+// dead with a packet still counted in flight: nothing is freed or destroyed
+// (a pending packet may still read its argument slot and write the caller's
+// buffers), so the caller must keep what those packets may write.
+bool pow_aql_close(pow_aql* a);
 // 0 = the last launch completed, 1 = still running, < 0 = the queue reported
 // an error (minus the HSA status).
 int pow_aql_status(const pow_aql* a);
 // One packet: `workgroups` x `wg_size` work-items of `kernel`, its explicit
 // arguments `args` (exactly the kernel's kernarg size).  0 = dispatched;
 // -1 = refused or failed (*why, if given, says why: a bad argument, a queue
-// error, or no free packet slot before `deadline_ns` on CLOCK_MONOTONIC).
+// error, or no free packet slot before `deadline_ns` on CLOCK_MONOTONIC).  A
+// failure after the packet's index was reserved leaves that slot INVALID on
+// the shared queue, which the packet processor cannot get past: the queue is
+// then marked dead (kQueueDead), so every context on it goes back to the HIP
+// launch path instead of timing out one by one.
 int pow_aql_dispatch(pow_aql* a, int kernel, uint32_t workgroups, uint32_t wg_size, const void* args,
                      uint32_t nbytes, uint64_t deadline_ns, std::string* why);
 // The watchdog's view of the context's last packet: completion-signal value,

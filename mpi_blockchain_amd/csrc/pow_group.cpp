@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <link.h>
 #include <rccl/rccl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <cstdint>
@@ -42,10 +43,11 @@
 
 namespace {
 
-// The RCCL entry points used here (rccl.h:187, 220, 260, 271, 339, 378, 389, 611).
+// The RCCL entry points used here (rccl.h:187, 204, 260, 271, 339, 362, 378, 389, 611).
 struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommInitRankConfig) comm_init_rank_config = nullptr;
+  decltype(&ncclCommGetAsyncError) get_async_error = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
@@ -97,14 +99,15 @@ const Rccl& rccl() {
       return x;
     }
     x.get_unique_id = (decltype(x.get_unique_id))dlsym(h, "ncclGetUniqueId");
-    x.comm_init_rank = (decltype(x.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    x.comm_init_rank_config = (decltype(x.comm_init_rank_config))dlsym(h, "ncclCommInitRankConfig");
+    x.get_async_error = (decltype(x.get_async_error))dlsym(h, "ncclCommGetAsyncError");
     x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
     x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
     x.comm_count = (decltype(x.comm_count))dlsym(h, "ncclCommCount");
     x.comm_cu_device = (decltype(x.comm_cu_device))dlsym(h, "ncclCommCuDevice");
     x.comm_abort = (decltype(x.comm_abort))dlsym(h, "ncclCommAbort");
-    if (!x.get_unique_id || !x.comm_init_rank || !x.comm_destroy || !x.all_reduce || !x.error_string ||
+    if (!x.get_unique_id || !x.comm_init_rank_config || !x.get_async_error || !x.comm_destroy || !x.all_reduce || !x.error_string ||
         !x.comm_count || !x.comm_cu_device || !x.comm_abort)
       snprintf(x.why, sizeof x.why, "RCCL lacks an entry point");
     Dl_info info;
@@ -133,6 +136,43 @@ int hip_fail(const char* what, hipError_t e) {
 
 constexpr size_t kMaxWords = 8;
 
+uint64_t now_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+// pow_group_init's deadline for every rank to join the communicator: 60 s, or
+// POW_GROUP_INIT_TIMEOUT_MS.
+uint64_t init_timeout_ns() {
+  if (const char* e = getenv("POW_GROUP_INIT_TIMEOUT_MS"))
+    if (const unsigned long long ms = strtoull(e, nullptr, 0)) return ms * 1000000ull;
+  return 60ull * 1000000000ull;
+}
+
+// The communicator is non-blocking (config.blocking = 0): RCCL calls on it may
+// return ncclInProgress while their work goes on in the background (joining
+// the peers at init, connecting to them at the first collective), and the
+// next call on the communicator or its stream must wait until the state
+// leaves ncclInProgress.  That wait is polled here against `deadline_ns`
+// (CLOCK_MONOTONIC); *late = true if it ran out first (the state is then
+// still ncclInProgress and the communicator must be aborted).
+ncclResult_t comm_settle(ncclComm_t c, uint64_t deadline_ns, bool* late) {
+  *late = false;
+  for (;;) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t r = rccl().get_async_error(c, &st);
+    if (r != ncclSuccess) return r;
+    if (st != ncclInProgress) return st;
+    if (now_ns() > deadline_ns) {
+      *late = true;
+      return ncclInProgress;
+    }
+    const timespec nap{0, 200000};  // 0.2 ms: a peer that is late by seconds costs no spinning core
+    nanosleep(&nap, nullptr);
+  }
+}
+
 }  // namespace
 
 struct pow_group {
@@ -146,7 +186,12 @@ struct pow_group {
   pow_board* board = nullptr; // the node's stop board (null: more than 64 ranks, or none available)
   uint32_t searches = 0;      // searches so far: every rank counts the same (the calls are collective)
   uint64_t shard_budget = 0;  // counters of the current round's largest shard (the all-reduce's watchdog budget)
-  bool broken = false;        // an all-reduce passed its deadline: ncclCommAbort, not ncclCommDestroy
+  // A collective failed or passed its deadline (or this rank left a round
+  // without joining its all-reduce): the ranks are out of step, so every later
+  // collective is refused, and destroy aborts the communicator (ncclCommAbort,
+  // not ncclCommDestroy) and frees the buffers only once the stream drained.
+  bool broken = false;
+  pow_group_search_info last{};  // the last pow_group_mine[_any] call (pow_group_last_search)
 };
 
 namespace {
@@ -154,8 +199,14 @@ namespace {
 // In-place all-reduce of n <= kMaxWords u64 (op = POW_REDUCE_*): RCCL on the
 // ctx's stream, or the caller's reduction of a custom group.
 int group_allreduce(pow_group* g, uint64_t* v, size_t n, int op) {
+  if (g->broken)
+    return pow_set_error(POW_ECOMM, "the group is broken (an earlier collective failed or ran out of time, or a rank "
+                                    "left a round without it): destroy it");
   if (g->reduce) {
-    if (g->reduce(g->reduce_user, v, n, op) != 0) return pow_set_error(POW_ECOMM, "custom reduction failed");
+    if (g->reduce(g->reduce_user, v, n, op) != 0) {
+      g->broken = true;
+      return pow_set_error(POW_ECOMM, "custom reduction failed");
+    }
     return POW_OK;
   }
   const ncclRedOp_t o = op == POW_REDUCE_MIN ? ncclMin : op == POW_REDUCE_MAX ? ncclMax : ncclSum;
@@ -163,16 +214,30 @@ int group_allreduce(pow_group* g, uint64_t* v, size_t n, int op) {
   if (e != hipSuccess) return hip_fail("hipSetDevice", e);
   hipStream_t st = (hipStream_t)pow_ctx_stream(g->ctx);
   memcpy(g->h_buf, v, n * sizeof(uint64_t));
-  if ((e = hipMemcpyAsync(g->d_buf, g->h_buf, n * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
+  if ((e = hipMemcpyAsync(g->d_buf, g->h_buf, n * 8, hipMemcpyHostToDevice, st)) != hipSuccess) {
+    g->broken = true;
     return hip_fail("hipMemcpyAsync", e);
-  ncclResult_t r = rccl().all_reduce(g->d_buf, g->d_buf, n, ncclUint64, o, g->comm, st);
-  if (r != ncclSuccess) return comm_fail("ncclAllReduce", r);
-  if ((e = hipMemcpyAsync(g->h_buf, g->d_buf, n * 8, hipMemcpyDeviceToHost, st)) != hipSuccess)
-    return hip_fail("hipMemcpyAsync", e);
+  }
   // Bounded (the watchdog): a peer that never joins this all-reduce (dead, or
   // stuck in its own launch) fails the call instead of hanging every rank.  A
   // peer still mining its shard of the round is waited for: the budget grows
   // with the round's shard (2 ns per counter, as the launch watchdog).
+  const uint64_t t0 = now_ns(), budget = 10ull * 1000000000ull + 2ull * g->shard_budget;
+  ncclResult_t r = rccl().all_reduce(g->d_buf, g->d_buf, n, ncclUint64, o, g->comm, st);
+  bool late = false;
+  if (r == ncclInProgress) r = comm_settle(g->comm, t0 + budget, &late);  // enqueued in the background
+  if (r != ncclSuccess) {
+    g->broken = true;
+    if (!late) return comm_fail("ncclAllReduce", r);
+    char buf[256];
+    snprintf(buf, sizeof buf, "ncclAllReduce: not enqueued within %.3f s (the communicator stayed in progress)",
+             (now_ns() - t0) * 1e-9);
+    return pow_set_error(POW_ECOMM, buf);
+  }
+  if ((e = hipMemcpyAsync(g->h_buf, g->d_buf, n * 8, hipMemcpyDeviceToHost, st)) != hipSuccess) {
+    g->broken = true;
+    return hip_fail("hipMemcpyAsync", e);
+  }
   if (pow_ctx_stream_wait(g->ctx, "ncclAllReduce", 2ull * g->shard_budget) != POW_OK) {
     g->broken = true;  // the communicator has an operation in flight: destroy aborts it
     char buf[512];
@@ -225,8 +290,14 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
                  pow_block* out, uint64_t* found_ctr, uint64_t* hashes_done, bool any) {
   const uint64_t big = (uint64_t)g->nranks << 30;
   const uint32_t tag = next_tag(g);
-  if (g->board)
+  pow_group_search_info& info = g->last;
+  info = pow_group_search_info{};
+  info.board_open = g->board != nullptr;
+  if (g->broken) return group_allreduce(g, nullptr, 0, POW_REDUCE_MIN);  // refused: says why
+  if (g->board) {
     if (int rc = pow_board_bind(g->ctx, g->board, g->rank, tag)) return rc;
+    info.board_bound = 1;
+  }
   struct Unbind {
     pow_group* g;
     ~Unbind() { pow_board_bind(g->ctx, nullptr, 0, 0); }
@@ -242,22 +313,50 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
     uint64_t v[3] = {UINT64_MAX, 1, 1};
     int local_rc = POW_OK;
     char local_err[512] = {0};
+    ++info.rounds;
+    info.local_found = 0;
     if (k) {
       pow_block tmp;
       uint64_t c = 0;
+      const uint64_t m0 = now_ns();
       local_rc = any ? pow_mine_any(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, nullptr)
                      : pow_mine(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, nullptr);
+      info.mine_end_ns = now_ns();
+      info.mine_ms += (info.mine_end_ns - m0) * 1e-6;
       st.add(g->ctx);
-      if (local_rc == 1) v[0] = c;
+      if (local_rc == 1) {
+        v[0] = c;
+        info.local_found = 1;
+      }
       if (local_rc < 0) {
         v[2] = 0;
         snprintf(local_err, sizeof local_err, "%s", pow_last_error());
       }
     }
+    if (local_rc < 0 && pow_ctx_wedged(g->ctx)) {
+      // This rank's launch is stuck on the ctx's stream (its watchdog fired):
+      // an all-reduce queued behind it would never run.  Leave at once with
+      // the real cause; the peers' all-reduce of this round fails at its own
+      // deadline, and the group is unusable from here on.
+      g->broken = true;
+      g->shard_budget = 0;
+      char buf[700];
+      snprintf(buf, sizeof buf, "%s; rank %d did not join the round's all-reduce (its stream holds the stuck launch)",
+               local_err, g->rank);
+      return pow_set_error(local_rc, buf);
+    }
     if (cancel_moved(cancel_word, epoch)) v[1] = 0;
+    const uint64_t a0 = now_ns();
     const int arc = group_allreduce(g, v, 3, POW_REDUCE_MIN);
+    info.allreduce_ms += (now_ns() - a0) * 1e-6;
     g->shard_budget = 0;
-    if (arc) return arc;
+    if (arc) {
+      if (local_rc >= 0) return arc;
+      // Both failed: the rank's own error is the cause, the collective's the consequence.
+      char buf[900];
+      snprintf(buf, sizeof buf, "%s (and the round's all-reduce failed: %s)", local_err, pow_last_error());
+      return pow_set_error(local_rc, buf);
+    }
     if (hashes_done) *hashes_done = st.s.hashes;
     pow_ctx_set_stats(g->ctx, st.s);
     if (v[2] == 0)  // every rank leaves the search together
@@ -331,7 +430,7 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
     return hip_fail("group buffers", e);
   }
   // The node's stop board: opened before the communicator, so that once
-  // ncclCommInitRank returns (every rank joined) every rank has it mapped and
+  // the communicator is up (every rank joined) every rank has it mapped and
   // its name can go.  Without one (> 64 ranks, no shared memory) the ranks
   // still stop together at the end of each round.
   char name[40];
@@ -339,12 +438,33 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
   if (nranks <= POW_BOARD_MAX_SLOTS && pow_board_open(name, nranks, &g->board) != POW_OK) g->board = nullptr;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
-  ncclResult_t r = R.comm_init_rank(&g->comm, nranks, u, rank);  // returns once every rank joined
+  // Non-blocking init under a deadline: ncclCommInitRank would wait for every
+  // rank with no bound, so one rank that fails before it joins (a GPU set-up
+  // error, a wrong device map, an exception) would hang the other N - 1
+  // forever.  Here they give up after init_timeout_ns(), abort the
+  // half-built communicator and report who waited for how long.
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const uint64_t t0 = now_ns(), budget = init_timeout_ns();
+  ncclResult_t r = R.comm_init_rank_config(&g->comm, nranks, u, rank, &cfg);
+  bool late = false;
+  if ((r == ncclSuccess || r == ncclInProgress) && g->comm) r = comm_settle(g->comm, t0 + budget, &late);
   pow_board_unlink(name);
   if (r != ncclSuccess) {
+    char buf[400];
+    const double el = (now_ns() - t0) * 1e-9;
+    if (late)
+      snprintf(buf, sizeof buf,
+               "ncclCommInitRankConfig: rank %d of %d on HIP device %d: not every rank joined within %.3f s "
+               "(elapsed %.3f s); communicator aborted",
+               rank, nranks, pow_ctx_device(ctx), budget * 1e-9, el);
+    else
+      snprintf(buf, sizeof buf, "ncclCommInitRankConfig: rank %d of %d on HIP device %d: %s (after %.3f s)", rank,
+               nranks, pow_ctx_device(ctx), R.error_string(r), el);
+    if (g->comm) (void)R.comm_abort(g->comm);
     g->comm = nullptr;
     pow_group_destroy(g);
-    return comm_fail("ncclCommInitRank", r);
+    return pow_set_error(POW_ECOMM, buf);
   }
   *out = g;
   return POW_OK;
@@ -388,8 +508,16 @@ void pow_group_destroy(pow_group* g) {
   }
   if (g->comm) (void)(g->broken ? rccl().comm_abort(g->comm) : rccl().comm_destroy(g->comm));
   pow_board_close(g->board);
-  if (g->d_buf) (void)hipFree(g->d_buf);
-  if (g->h_buf) (void)hipHostFree(g->h_buf);
+  // hipFree waits for the whole device: after a failed collective (or a stuck
+  // launch of the ctx) free the staging buffers only once a bounded wait saw
+  // the ctx's stream drain, and leak them otherwise, as pow_destroy does.
+  bool drained = true;
+  if (g->ctx && (g->d_buf || g->h_buf) && (g->broken || pow_ctx_wedged(g->ctx)))
+    drained = !pow_ctx_wedged(g->ctx) && pow_ctx_stream_wait(g->ctx, "pow_group_destroy", 0) == POW_OK;
+  if (drained) {
+    if (g->d_buf) (void)hipFree(g->d_buf);
+    if (g->h_buf) (void)hipHostFree(g->h_buf);
+  }
   delete g;
 }
 
@@ -412,6 +540,13 @@ int pow_group_info(const pow_group* g, int* comm_count, int* comm_device) {
   }
   if (comm_count) *comm_count = n;
   if (comm_device) *comm_device = dev;
+  return POW_OK;
+}
+
+int pow_group_last_search(const pow_group* g, pow_group_search_info* out) {
+  if (!g || !out) return pow_set_error(POW_EINVAL, "null");
+  *out = g->last;
+  out->board_open = g->board != nullptr;
   return POW_OK;
 }
 

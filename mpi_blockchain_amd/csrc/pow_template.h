@@ -190,6 +190,9 @@ void pow_build_consts(const struct pow_block* tmpl, PowConsts* out);
 // Library-internal accessors of a context (used by pow_group.cpp).
 int pow_ctx_device(const struct pow_ctx* ctx);
 void* pow_ctx_stream(const struct pow_ctx* ctx);  // the ctx's hipStream_t
+// A watchdog of the ctx fired: a launch may still be queued (never reuse the
+// stream, never free what it may write).
+bool pow_ctx_wedged(const struct pow_ctx* ctx);
 // Bounded wait for everything queued on the ctx's stream (the watchdog):
 // POW_OK, or POW_EHIP naming `what` once `budget_ns` past the base deadline
 // has gone by without the stream draining.

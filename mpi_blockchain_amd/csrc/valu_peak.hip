@@ -18,6 +18,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include "../../include/pow_gpu.h"
@@ -94,32 +96,55 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   int rt_khz = 100000;
   (void)hipDeviceGetAttribute(&rt_khz, hipDeviceAttributeWallClockRate, device);
   const unsigned grid = (unsigned)prop.multiProcessorCount * 8u;  // 32 waves per CU
+  // Every launch, event and copy on a stream of this call's own (never HIP's
+  // null stream, which would give the calling process one hardware queue more
+  // for as long as it lives: DESIGN.md §7, "Queue pressure"), and every wait
+  // bounded (30 s).  A wait that runs out leaks the buffers instead of freeing
+  // them under a kernel that may still write them.
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return POW_EHIP;
   uint32_t* out = nullptr;
   unsigned long long* stamps = nullptr;
-  if (hipMalloc(&out, 4) != hipSuccess) return POW_EHIP;
-  if (hipMalloc(&stamps, (size_t)grid * 16) != hipSuccess) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (hipMalloc(&out, 4) != hipSuccess || hipMalloc(&stamps, (size_t)grid * 16) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
     (void)hipFree(out);
+    (void)hipFree(stamps);
+    (void)hipStreamDestroy(st);
     return POW_EHIP;
   }
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
+  auto wait = [&](hipEvent_t ev) {  // bounded: POW_OK, POW_EHIP on an error or after 30 s
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return POW_EHIP;
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    return q == hipSuccess ? POW_OK : POW_EHIP;
+  };
   float best = 1e30f;
   double best_clock = 0;
   std::vector<unsigned long long> h(2 * (size_t)grid);
   int rc = POW_OK;
+  bool drained = true;
   for (int rep = 0; rep < 4 && rc == POW_OK; ++rep) {  // rep 0 warms up clocks
-    (void)hipEventRecord(e0, 0);
+    (void)hipEventRecord(e0, st);
     if (kind == POW_VALU_MIX)
-      hipLaunchKernelGGL(valu_rate_kernel<POW_VALU_MIX>, dim3(grid), dim3(256), 0, 0, 0x1234u + rep, out, stamps);
+      hipLaunchKernelGGL(valu_rate_kernel<POW_VALU_MIX>, dim3(grid), dim3(256), 0, st, 0x1234u + rep, out, stamps);
     else if (kind == POW_VALU_FULL)
-      hipLaunchKernelGGL(valu_rate_kernel<POW_VALU_FULL>, dim3(grid), dim3(256), 0, 0, 0x1234u + rep, out, stamps);
+      hipLaunchKernelGGL(valu_rate_kernel<POW_VALU_FULL>, dim3(grid), dim3(256), 0, st, 0x1234u + rep, out, stamps);
     else
-      hipLaunchKernelGGL(valu_rate_kernel<POW_VALU_HALF>, dim3(grid), dim3(256), 0, 0, 0x1234u + rep, out, stamps);
-    (void)hipEventRecord(e1, 0);
-    if (hipEventSynchronize(e1) != hipSuccess ||
-        hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+      hipLaunchKernelGGL(valu_rate_kernel<POW_VALU_HALF>, dim3(grid), dim3(256), 0, st, 0x1234u + rep, out, stamps);
+    (void)hipEventRecord(e1, st);
+    if (hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess) {
       rc = POW_EHIP;
+      drained = wait(e1) == POW_OK;
+      break;
+    }
+    if ((rc = wait(e1)) != POW_OK || (rc = hipStreamSynchronize(st) == hipSuccess ? POW_OK : POW_EHIP) != POW_OK) {
+      drained = hipEventQuery(e1) == hipSuccess;
       break;
     }
     float ms = 0;
@@ -135,10 +160,12 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
       best_clock = clk.empty() ? 0 : clk[clk.size() / 2];
     }
   }
+  if (!drained) return rc;  // a launch may still be running: keep its stream, events and buffers
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipFree(out);
   (void)hipFree(stamps);
+  (void)hipStreamDestroy(st);
   if (rc != POW_OK) return rc;
   const double wave_instr = (double)grid * 4.0 * VP_ITERS(kind) * instrs_per_iter(kind);
   res->lane_ops_per_s = wave_instr * 64.0 / (best * 1e-3);

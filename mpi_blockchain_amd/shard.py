@@ -29,7 +29,8 @@ import ctypes
 import os
 import uuid
 
-from ._lib import POW_REDUCE_MAX, POW_REDUCE_MIN, POW_REDUCE_SUM, REDUCE_FN, Block, check, load
+from ._lib import (POW_REDUCE_MAX, POW_REDUCE_MIN, POW_REDUCE_SUM, REDUCE_FN, Block, GroupSearchInfo, check,
+                   load)
 
 _U64 = 1 << 64
 _HALF = 1 << 63
@@ -94,6 +95,16 @@ class _Group:
         n, dev = ctypes.c_int(), ctypes.c_int()
         check(self.L.pow_group_info(self.g, ctypes.byref(n), ctypes.byref(dev)), self.L)
         return {"comm_count": n.value, "comm_device": dev.value}
+
+    def last_search(self) -> dict:
+        """This rank's part in the group's last :meth:`mine`
+        (pow_group_last_search): whether the stop board was open and bound,
+        the rounds, whether this rank's own launch found the solution, when
+        that launch returned (CLOCK_MONOTONIC ns, = time.monotonic_ns()), and
+        the wall ms in its launches and in the rounds' all-reduces."""
+        i = GroupSearchInfo()
+        check(self.L.pow_group_last_search(self.g, ctypes.byref(i)), self.L)
+        return {k: getattr(i, k) for k, _ in GroupSearchInfo._fields_}
 
     def close(self) -> None:
         if self.g:

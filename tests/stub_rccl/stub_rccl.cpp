@@ -1,6 +1,7 @@
-// TEST INFRASTRUCTURE ONLY: a stand-in for the eight RCCL entry points that
-// mpi_blockchain_amd/csrc/pow_group.cpp dlopens (rccl.h:187, 220, 260, 271,
-// 339, 378, 389, 611), reducing over POSIX shared memory instead of xGMI.
+// TEST INFRASTRUCTURE ONLY: a stand-in for the RCCL entry points that
+// mpi_blockchain_amd/csrc/pow_group.cpp dlopens (rccl.h:187, 204, 220, 260,
+// 271, 339, 362, 378, 389, 611), reducing over POSIX shared memory instead of
+// xGMI.
 //
 // RCCL refuses two ranks on one GPU, and a test box has one GPU, so
 // pow_group_init's RCCL leg (the board opened before ncclCommInitRank and
@@ -12,6 +13,10 @@
 // never loaded by the shipped libpow_gpu.so, which has no such hook.
 //
 // Semantics kept from RCCL: ncclCommInitRank blocks until all nranks joined;
+// ncclCommInitRankConfig with config->blocking = 0 returns ncclInProgress at
+// once and ncclCommGetAsyncError reports ncclInProgress until every rank has
+// joined (then ncclSuccess); ncclCommAbort tears down a communicator in any
+// state;
 // ncclAllReduce takes device buffers and is ordered on the caller's stream
 // (the stub synchronises the stream, reduces on the host, and writes the
 // result back on the same stream).  Only what pow_group uses is supported:
@@ -45,6 +50,7 @@ struct Shared {
 };
 
 std::atomic<uint64_t> g_allreduce_calls{0};
+std::atomic<uint64_t> g_aborts{0};
 
 double now_s() {
   timespec t;
@@ -69,6 +75,8 @@ struct ncclComm {
   Shared* sh = nullptr;
   int nranks = 0, rank = 0;
   int device = -1;  // the HIP device current at ncclCommInitRank (as RCCL binds it)
+  bool ready = false;  // every rank joined (a non-blocking init is in progress until then)
+  char name[48] = {0};
 };
 
 namespace {
@@ -96,6 +104,8 @@ extern "C" {
 // How many all-reduces this process ran through the stub (tests check that the
 // stub, not RCCL, carried the group's collectives).
 uint64_t pow_stub_rccl_allreduce_calls(void) { return g_allreduce_calls.load(); }
+// How many communicators this process aborted (the init-deadline test).
+uint64_t pow_stub_rccl_aborts(void) { return g_aborts.load(); }
 
 ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
   if (!id) return ncclInvalidArgument;
@@ -108,7 +118,10 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
   return ncclSuccess;
 }
 
-ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank) {
+namespace {
+
+// Map the id's segment and count this rank in; *out = the communicator, not yet ready.
+ncclResult_t comm_join(ncclComm_t* comm, int nranks, const ncclUniqueId& id, int rank) {
   if (!comm || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) return ncclInvalidArgument;
   if (memcmp(id.internal, kMagic, sizeof kMagic) != 0) return ncclInvalidArgument;  // not a stub id
   *comm = nullptr;
@@ -128,33 +141,75 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
   c->sh = (Shared*)p;  // a fresh object is zero-filled: all counters 0
   c->nranks = nranks;
   c->rank = rank;
+  snprintf(c->name, sizeof c->name, "%s", name);
   if (hipGetDevice(&c->device) != hipSuccess) c->device = -1;
-  // As RCCL: return once every rank has joined.
   c->sh->joined.fetch_add(1, std::memory_order_acq_rel);
+  *comm = c;
+  return ncclSuccess;
+}
+
+// Every rank has joined: the communicator is ready, and the name can go.
+bool comm_ready(ncclComm* c) {
+  if (!c->ready && c->sh->joined.load(std::memory_order_acquire) >= (uint32_t)c->nranks) {
+    c->ready = true;
+    shm_unlink(c->name);  // every rank has it mapped; nothing is left in /dev/shm
+  }
+  return c->ready;
+}
+
+}  // namespace
+
+ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank) {
+  ncclResult_t r = comm_join(comm, nranks, id, rank);
+  if (r != ncclSuccess) return r;
+  ncclComm* c = *comm;
+  // As RCCL: return once every rank has joined.
   const double t0 = now_s();
-  while (c->sh->joined.load(std::memory_order_acquire) < (uint32_t)nranks) {
+  while (!comm_ready(c)) {
     if (now_s() - t0 > kTimeoutS) {
-      munmap(p, sizeof(Shared));
+      munmap(c->sh, sizeof(Shared));
       delete c;
+      *comm = nullptr;
       return ncclSystemError;
     }
     pause_us(50);
   }
-  shm_unlink(name);  // every rank has it mapped; nothing is left in /dev/shm
-  *comm = c;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank, ncclConfig_t* config) {
+  if (config && config->magic != 0xcafebeef) return ncclInvalidArgument;
+  if (!config || config->blocking != 0) return ncclCommInitRank(comm, nranks, id, rank);
+  ncclResult_t r = comm_join(comm, nranks, id, rank);
+  if (r != ncclSuccess) return r;
+  return comm_ready(*comm) ? ncclSuccess : ncclInProgress;
+}
+
+ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
+  if (!comm || !asyncError) return ncclInvalidArgument;
+  *asyncError = comm_ready(comm) ? ncclSuccess : ncclInProgress;
   return ncclSuccess;
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
+  if (!comm->ready) return ncclInvalidUsage;  // RCCL: an initialising communicator is aborted, not destroyed
   munmap(comm->sh, sizeof(Shared));
   delete comm;
   return ncclSuccess;
 }
 
 // As RCCL's: tear the communicator down without waiting for operations in
-// flight (the stub has none once a call returns).
-ncclResult_t ncclCommAbort(ncclComm_t comm) { return ncclCommDestroy(comm); }
+// flight (the stub has none once a call returns), also one whose non-blocking
+// init never completed (its segment's name is removed: nobody else will).
+ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  if (!comm->ready) shm_unlink(comm->name);
+  munmap(comm->sh, sizeof(Shared));
+  delete comm;
+  g_aborts.fetch_add(1);
+  return ncclSuccess;
+}
 
 ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
   if (!comm || !count) return ncclInvalidArgument;
@@ -181,6 +236,7 @@ const char* ncclGetErrorString(ncclResult_t r) {
 ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
                            ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
   if (!comm || datatype != ncclUint64 || count > kMaxWords) return ncclInvalidArgument;
+  if (!comm->ready) return ncclInvalidUsage;
   if (op != ncclMin && op != ncclMax && op != ncclSum) return ncclInvalidArgument;
   uint64_t v[kMaxWords] = {0};
   // The operand was staged on `stream` (pow_group: hipMemcpyAsync H2D): read it

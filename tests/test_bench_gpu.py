@@ -114,12 +114,32 @@ def run_rehearsal(n: int, transport: str = "gloo") -> dict:
     if transport == "rccl_stub":
         assert topo["rccl_library"].endswith("tests/stub_rccl/libstub_rccl.so"), topo
     assert "cpu_baseline" not in d and "ladder" not in d  # rank-0-at-N=1-only extras
+    # per-rank attribution of the step: kernel + all-reduce <= the rank's own step (noise aside)
+    tm = d["timing"]
+    assert len(tm["per_rank_kernel_ms"]) == n and len(tm["allreduce_ms_per_step"]) == n, tm
+    for k, a, st in zip(tm["per_rank_kernel_ms"], tm["allreduce_ms_per_step"], tm["per_rank_step_ms"]):
+        assert k > 0 and a > 0 and k + a <= 1.05 * st + 1.0, tm
+        assert max(st, k + a) <= 1.05 * d["ms_per_step"] + 1.0, tm  # nobody's step exceeds the job's
+    assert tm["imbalance"] >= 1.0 and d["imbalance"] == tm["imbalance"], tm
+    # the stop board: open and bound on every rank, and peers stopped by it (not at the round's end)
+    bd = gs["board"]
+    assert [r["rank"] for r in bd["per_rank"]] == list(range(n)), bd
+    assert all(r["board_open"] and r["board_bound_every_search"] for r in bd["per_rank"]), bd
+    assert bd["all_ranks_board"] is True and bd["stop_latency_samples"] >= 15, bd
+    assert bd["peers_stopped_by_board"] is True, bd
     # config 5 at the job's size: mpiexec -np n pow_node (here all on the one GPU)
     pr = d["protocol"]
     assert pr["ranks"] == n
     for key in ("d9", "d25", "d5_forced_fork"):
         assert pr[key]["rc"] == 0 and pr[key]["chains_consistent"] and pr[key]["chains_complete"] >= 1, pr
         assert pr[key]["hard_errors"] == 0, pr
+        # every pow_node rank said where it mined: here all on the one GPU (a rehearsal: reported, not failed)
+        pl = pr[key]["placement"]
+        assert [x["rank"] for x in pl["devices"]] == list(range(n)) and pl["all_ranks_reported"], pl
+        assert all(x["device"] == 0 and x["local_rank_from"] == "MPI_LOCALRANKID" for x in pl["devices"]), pl
+        assert pl["distinct_gpus"] is False and pl["rehearsal"] is True and pl["ok"] is True, pl
+        assert pl["no_local_rank_warnings"] == [], pl
+    assert pr["ok"] is True and pr["distinct_gpus"] is False, pr
     assert pr["d5_forced_fork"]["blocks_mined"] >= n and pr["d5_forced_fork"]["fork_events"] >= 1, pr
     return d
 
@@ -149,3 +169,37 @@ def test_bench_eight_rank_rehearsal():
     assert all(c["ok"] is True and c["fingerprint_ok"] is True for c in chk.values()), chk
     assert d["parity"]["count_ok"] is True and d["parity"]["fingerprint_ok"] is True
     assert d["parity"]["solutions_all_ranks"] > 8 * 8_000_000
+
+
+def test_bench_rank_dies_at_group_init():
+    """The first N > 1 contact, broken on purpose: rank 1 of 2 dies after its
+    GPU set-up, as the group forms (BENCH_TEST_FAIL).  Rank 0, waiting for it
+    there, is stopped by torch.distributed.run; both ranks leave their
+    `bench_rank_failure` line naming the phase, no result line is printed, and
+    the job ends non-zero in seconds, not at the driver's 600 s limit."""
+    import socket
+    import time
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, BENCH_REHEARSAL="1", BENCH_REHEARSAL_TRANSPORT="rccl_stub", BENCH_TEST_FAIL="1:group_init")
+    t = time.monotonic()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    wall = time.monotonic() - t
+    assert p.returncode != 0
+    fails = {}
+    for ln in p.stderr.splitlines():
+        if ln.startswith('{"bench_rank_failure"'):
+            f = json.loads(ln)["bench_rank_failure"]
+            fails[f["rank"]] = f
+    assert sorted(fails) == [0, 1], p.stderr[-3000:]
+    assert fails[1]["phase"] == "group_init" and fails[1]["exit_code"] == 6, fails[1]
+    assert [x[0] for x in fails[1]["phases_done"]] == ["import", "process_group", "device_init"], fails[1]
+    assert fails[0]["phase"] == "group_init" and fails[0]["exit_code"] == 143, fails[0]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert wall < 150, wall

@@ -264,3 +264,62 @@ def test_topology_check():
     assert bench.topology_check(cpx, 8, None, "rccl", False)["distinct_gpus"]
     missing = [{k: v for k, v in x.items() if k != "group_comm_count"} for x in good]
     assert not bench.topology_check(missing, 8, None, "rccl", False)["ok"]
+
+
+def _node_line(rank, size, dev, pci, host="h", frm="MPI_LOCALRANKID"):
+    return ('pow_node device {"rank": %d, "size": %d, "device": %d, "pci": "%s", "host": "%s", "pid": 1, '
+            '"local_rank": %d, "local_rank_from": "%s", "visible_gpus": 8}' % (rank, size, dev, pci, host, rank, frm))
+
+
+def test_node_placement():
+    """Config 5's placement check (bench.node_placement) from pow_node's
+    start-up lines: one rank per distinct GPU passes; all ranks on one GPU
+    fail a real run and pass a rehearsal; a missing line or a no-local-rank
+    warning fails both."""
+    good = "\n".join(["[MPI] Lanzando proceso 0"] + [_node_line(r, 8, r, f"0000:{0x05 + r:02x}:00.0")
+                                                      for r in range(8)])
+    p = bench.node_placement(good, 8, False)
+    assert p["ok"] and p["distinct_gpus"] and p["all_ranks_reported"] and [d["device"] for d in p["devices"]] == \
+        list(range(8)), p
+    shared = "\n".join(_node_line(r, 8, 0, "0000:05:00.0") for r in range(8))
+    p = bench.node_placement(shared, 8, False)
+    assert not p["ok"] and not p["distinct_gpus"] and "distinct" in p["failed"], p
+    assert bench.node_placement(shared, 8, True)["ok"]
+    missing = "\n".join(_node_line(r, 8, r, f"0000:{r:02x}:00.0") for r in range(7))
+    p = bench.node_placement(missing, 8, False)
+    assert not p["ok"] and not p["all_ranks_reported"], p
+    warned = "\n".join([_node_line(r, 2, 0, "0000:05:00.0", frm="none") for r in range(2)] +
+                       ["pow_node: rank 1 of 2: no node-local rank in the environment (MPI_LOCALRANKID, ...)"])
+    p = bench.node_placement(warned, 2, True)
+    assert not p["ok"] and p["no_local_rank_warnings"] == [1] and "node-local" in p["failed"], p
+    # PCI addresses compare case-insensitively; two hosts with the same address are two GPUs
+    two = "\n".join([_node_line(0, 2, 0, "0000:05:00.0", host="a"), _node_line(1, 2, 0, "0000:05:00.0", host="b")])
+    assert bench.node_placement(two, 2, False)["ok"]
+
+
+def test_timing_block():
+    """Per-rank attribution of the N > 1 step: kernel, all-reduce, own step,
+    what is left of the job's step, and the kernel imbalance (max / min)."""
+    ranks = [bench.rank_timing(r, [470.0 + r, 470.0 + r], [0.2, 0.3], 0.4715 * 2, 2) for r in range(4)]
+    assert ranks[3] == {"rank": 3, "kernel_ms": 473.0, "allreduce_ms": 0.25, "step_ms": 471.5}
+    t = bench.timing_block(ranks, 474.0)
+    assert t["per_rank_kernel_ms"] == [470.0, 471.0, 472.0, 473.0]
+    assert t["allreduce_ms_per_step"] == [0.25] * 4 and t["slowest_kernel_rank"] == 3
+    assert abs(t["imbalance"] - 473.0 / 470.0) < 1e-4
+    assert t["per_rank_other_ms"][0] == round(474.0 - 470.0 - 0.25, 3)
+    one = bench.timing_block([bench.rank_timing(0, [469.5], [], 0.47, 1)], 470.0)
+    assert one["imbalance"] == 1.0 and one["allreduce_ms_per_step"] == [0.0]
+
+
+def test_board_summary():
+    """The stop board works when every rank had it bound and peers stop within
+    tens of us of the finder; a missing board, or peers that run out their
+    shards (~470 ms), say so."""
+    ok_rank = {"board_open": True, "board_bound_every_search": True}
+    b = bench.board_summary([dict(ok_rank, rank=r) for r in range(8)], [35.0, 40.0, 80.0], 8)
+    assert b["all_ranks_board"] and b["peers_stopped_by_board"] and b["stop_latency_us_median"] == 40.0
+    b = bench.board_summary([dict(ok_rank, rank=0), dict(ok_rank, rank=1, board_open=False)], [30.0], 2)
+    assert not b["all_ranks_board"] and b["peers_stopped_by_board"] is False
+    b = bench.board_summary([dict(ok_rank, rank=r) for r in range(2)], [460_000.0, 470_000.0], 2)
+    assert b["all_ranks_board"] and b["peers_stopped_by_board"] is False  # bound, but not stopping peers
+    assert bench.board_summary([dict(ok_rank, rank=0)], [], 1)["peers_stopped_by_board"] is None

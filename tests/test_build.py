@@ -387,3 +387,136 @@ def test_k1_instruction_budget_guard(isa):
                 or re.search(r"\bs\d+\b|\bs\[", ln)]
         assert abs(len(lines) - 4839) <= 48, (variant, len(lines))
         assert len(half) <= 2774, (variant, len(half))
+
+
+# ---- queue pressure guard: no HIP null-stream use in the library's sources ----
+# A process that touches HIP's null stream holds one hardware queue more for
+# the rest of its life; with 6-8 ranks per GPU that tipped the GPU past its
+# compute queue slots and a launch waited 10 s for a queue (round 5,
+# DESIGN.md §7 "Queue pressure").  Every copy, fill, event and launch must name
+# a stream of its own.
+NULL_STREAM_FREE = ("hipMemcpy", "hipMemset", "hipMemsetD8", "hipMemsetD16", "hipMemsetD32", "hipMemcpy2D",
+                    "hipMemcpy3D", "hipMemcpyToSymbol", "hipMemcpyFromSymbol", "hipMemcpyHtoD", "hipMemcpyDtoH",
+                    "hipMemcpyDtoD", "hipMemcpyPeer", "hipDeviceSynchronize")
+# call -> (index of its stream argument, number of arguments with the stream given)
+STREAM_ARG = {"hipMemcpyAsync": (4, 5), "hipMemsetAsync": (3, 4), "hipMemsetD32Async": (3, 4),
+              "hipMemcpyToSymbolAsync": (5, 6), "hipMemcpyFromSymbolAsync": (5, 6), "hipMemcpy2DAsync": (7, 8),
+              "hipMemcpyPeerAsync": (5, 6), "hipEventRecord": (1, 2), "hipLaunchKernelGGL": (4, None),
+              "hipExtLaunchKernelGGL": (4, None), "hipLaunchKernel": (5, 6), "hipLaunchCooperativeKernel": (5, 6),
+              "hipModuleLaunchKernel": (9, None), "hipStreamSynchronize": (0, 1), "hipStreamQuery": (0, 1),
+              "hipStreamWaitEvent": (0, 3), "hipGraphLaunch": (1, 2)}
+NULL_STREAMS = {"0", "0u", "nullptr", "NULL", "hipStreamDefault", "hipStreamLegacy", "hipStreamPerThread",
+                "(hipStream_t)0", "hipStream_t(0)", "hipStream_t{}", "(hipStream_t) 0"}
+SHIPPED_SOURCES = [os.path.join(CSRC, f) for f in ("pow_api.cpp", "pow_aql.cpp", "pow_board.cpp", "pow_group.cpp",
+                                                    "pow_kernels.hip", "pow_sort.hip", "valu_peak.hip",
+                                                    "pow_test_kernels.hip", "pow_template.h", "sha256_dev.h",
+                                                    "pow_aql.h", os.path.join("node", "pow_node.cpp"))] + \
+    [os.path.join(ROOT, "tests", "stub_rccl", "stub_rccl.cpp")]
+
+
+def _strip_comments_and_strings(text: str) -> str:
+    """C/C++ source with comments and string/char literals blanked (newlines kept)."""
+    out, i, n = [], 0, len(text)
+    while i < n:
+        c = text[i]
+        if text.startswith("//", i):
+            j = text.find("\n", i)
+            i = n if j < 0 else j
+        elif text.startswith("/*", i):
+            j = text.find("*/", i + 2)
+            j = n if j < 0 else j + 2
+            out.append("".join(ch if ch == "\n" else " " for ch in text[i:j]))
+            i = j
+        elif c in "\"'":
+            j = i + 1
+            while j < n and text[j] != c:
+                j += 2 if text[j] == "\\" else 1
+            out.append(c + " " * (min(j, n) - i - 1) + c)
+            i = j + 1
+        else:
+            out.append(c)
+            i += 1
+    return "".join(out)
+
+
+def _call_args(text: str, open_paren: int) -> list[str] | None:
+    """Top-level arguments of the call whose '(' is at `open_paren`."""
+    depth, args, cur = 0, [], []
+    for ch in text[open_paren:]:
+        if ch in "([{":
+            depth += 1
+            if depth == 1:
+                continue
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                args.append("".join(cur).strip())
+                return [a for a in args if a] if args != [""] else []
+        elif ch == "," and depth == 1:
+            args.append("".join(cur).strip())
+            cur = []
+            continue
+        cur.append(ch)
+    return None
+
+
+def null_stream_calls(text: str) -> list[tuple[int, str]]:
+    """(line, call) of every HIP call in `text` that runs on the null stream:
+    a null-stream-only API, a stream argument left out or given as 0/nullptr,
+    or a <<<...>>> launch without a stream."""
+    src = _strip_comments_and_strings(text)
+    bad = []
+    line = lambda pos: src.count("\n", 0, pos) + 1  # noqa: E731
+    for m in re.finditer(r"\b(hip\w+)\s*\(", src):
+        name = m.group(1)
+        if name in NULL_STREAM_FREE:
+            bad.append((line(m.start()), name))
+        elif name in STREAM_ARG:
+            args = _call_args(src, m.end() - 1)
+            if args is None:
+                continue
+            idx, full = STREAM_ARG[name]
+            if len(args) <= idx or (full is not None and len(args) < full):
+                bad.append((line(m.start()), f"{name} without a stream"))
+            elif re.sub(r"\s+", " ", args[idx]) in NULL_STREAMS:
+                bad.append((line(m.start()), f"{name} on stream {args[idx]}"))
+    for m in re.finditer(r"<<<(.*?)>>>", src, re.S):
+        cfg = _call_args("(" + m.group(1) + ")", 0) or []
+        if len(cfg) < 4 or re.sub(r"\s+", " ", cfg[3]) in NULL_STREAMS:
+            bad.append((line(m.start()), "<<<>>> launch on the null stream"))
+    return bad
+
+
+def test_no_null_stream_in_library_sources():
+    found = {}
+    for p in SHIPPED_SOURCES:
+        hits = null_stream_calls(open(p).read())
+        if hits:
+            found[os.path.relpath(p, ROOT)] = hits
+    assert not found, found
+
+
+def test_null_stream_check_catches_seeded_calls():
+    """The guard fails on each form a null-stream call can take (seeded into
+    the real valu_peak.hip), and passes the stream-explicit forms."""
+    base = open(os.path.join(CSRC, "valu_peak.hip")).read()
+    assert null_stream_calls(base) == []
+    seeds = ["hipMemcpy(h, d, 8, hipMemcpyDeviceToHost);",
+             "hipMemset(d, 0, 8);",
+             "hipDeviceSynchronize();",
+             "hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost);",
+             "hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, 0);",
+             "hipMemsetAsync(d, 0, 8);",
+             "hipEventRecord(e0);",
+             "hipEventRecord(e0, nullptr);",
+             "hipLaunchKernelGGL((k<1, 2>), dim3(1), dim3(64), 0, 0, a, b);",
+             "k<<<dim3(1), dim3(64)>>>(a);",
+             "k<<<1, 64, 0, 0>>>(a);",
+             "hipStreamSynchronize(0);"]
+    for seed in seeds:
+        hits = null_stream_calls(base + "\nvoid seeded() {\n  " + seed + "\n}\n")
+        assert len(hits) == 1, (seed, hits)
+    for ok in ["hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);", "hipEventRecord(e0, ctx->stream);",
+               "hipLaunchKernelGGL((k<1, 2>), dim3(1), dim3(64), 0, stream, a, b);", "k<<<1, 64, 0, st>>>(a);",
+               "// hipMemcpy(h, d, 8, hipMemcpyDeviceToHost); in a comment", 'puts("hipMemset(d, 0, 8)");']:
+        assert null_stream_calls("void f() {\n  " + ok + "\n}\n") == [], ok

@@ -90,3 +90,53 @@ def test_board_example_stops_peer(board_exe):
                        env=dict(os.environ, POW_GRID_PER_CU="4"))
     assert p.returncode == 0, p.stdout + p.stderr
     assert "A: rc 1 " in p.stdout and "B: rc 0 " in p.stdout, p.stdout
+
+
+def _deadline_exe(tmp_path_factory, lib: str) -> str:
+    from mpi_blockchain_amd.build import build, build_test_stub
+
+    build()
+    build_test_stub()
+    out = str(tmp_path_factory.mktemp("cd") / f"group_init_deadline_{lib}")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-D_POSIX_C_SOURCE=200809L", "-I",
+                    os.path.join(ROOT, "include"), os.path.join(ROOT, "examples", "group_init_deadline.c"), "-L", PKG,
+                    f"-l{lib}", f"-Wl,-rpath,{PKG}", "-o", out], check=True)
+    return out
+
+
+@pytest.fixture(scope="module")
+def deadline_exes(tmp_path_factory):
+    return {lib: _deadline_exe(tmp_path_factory, lib) for lib in ("pow_gpu", "pow_gpu_test")}
+
+
+def test_group_init_deadline_example_builds(deadline_exes):
+    assert all(os.path.exists(p) for p in deadline_exes.values())
+
+
+def _shm_names(prefix: str) -> set:
+    return {f for f in os.listdir("/dev/shm") if f.startswith(prefix)} if os.path.isdir("/dev/shm") else set()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl_stub", "rccl"])
+def test_group_init_deadline(deadline_exes, transport):
+    """A rank that never calls pow_group_init: its peer's pow_group_init returns
+    POW_ECOMM after the 3 s deadline (non-blocking ncclCommInitRankConfig
+    polled by ncclCommGetAsyncError, then ncclCommAbort) instead of waiting
+    forever, and the context stays usable (a one-rank group then mines S0 at
+    d = 21 to 2392323).  rccl_stub: the test library with the stand-in RCCL;
+    rccl: the shipped library with RCCL itself (torch's copy is not loaded
+    here: librccl.so.1 from the library path)."""
+    from mpi_blockchain_amd.build import STUB_LIB
+
+    env = dict(os.environ)
+    if transport == "rccl_stub":
+        env["POW_TEST_RCCL_LIB"] = STUB_LIB
+    exe = deadline_exes["pow_gpu_test" if transport == "rccl_stub" else "pow_gpu"]
+    before = _shm_names("pow_")
+    p = subprocess.run(["timeout", "-k", "5", "90", exe, "3000"], capture_output=True, text=True, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr[-3000:]
+    assert "lonely rank 0 of 2: rc -5 after" in p.stdout and "not every rank joined within 3.000 s" in p.stdout, \
+        p.stdout
+    assert "one-rank group: counter 2392323," in p.stdout and p.stdout.rstrip().endswith("ok"), p.stdout
+    assert _shm_names("pow_") <= before  # the board's and the stand-in's segments are gone

@@ -20,12 +20,14 @@
 #   ttb D L...       time-to-block A/B at difficulty D (tools/ab_ttb, 301 templates)
 #   k2_trace         rocprofv3 HIP API + kernel trace of 200 pow_hash_block calls
 #   pmc_onewave      PMC (clock, wave cycles, VALU) of K2' and of K1' at d = 9
+#   sanitize         host ASan/UBSan then TSan runs of the C ABI, the node and pow_group_init's deadline
+#                    (build them first, here: tools/host_sanitize.sh build && tools/host_sanitize.sh tsan-build)
 # A/B library lists end at the next step name.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 S="$R/tools/gpu_step.sh"
 L="$R/mpi_blockchain_amd/libpow_gpu.so"
-STEPS=" tests smoke bench profile fuzz fuzz_big soak_mixed queue_pressure queue_ab ab_k1 ab_k2 ttb k2_trace pmc_onewave "
+STEPS=" tests smoke bench profile fuzz fuzz_big soak_mixed queue_pressure queue_ab ab_k1 ab_k2 ttb k2_trace pmc_onewave sanitize "
 libs() {  # the library arguments of an A/B step
   LIBS=()
   while [ $# -gt 0 ] && [[ "$STEPS" != *" $1 "* ]]; do LIBS+=("$1"); shift; done
@@ -57,6 +59,8 @@ while [ $# -gt 0 ]; do
           --kernel-trace -f csv --kernel-include-regex pow_hash_one -d "$R/gpurun_out/k2_pmc" -o run -- "$R/tools/ab_k2" 1 "$L" &&
         $S lat_pmc 90 timeout -s KILL 60 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES \
           --kernel-trace -f csv --kernel-include-regex pow_search_lat -d "$R/gpurun_out/lat_pmc" -o run -- "$R/tools/ab_ttb" 9 101 "$L") \
+        || exit $? ;;
+    sanitize) $S asan 600 bash "$R/tools/host_sanitize.sh" run && $S tsan 600 bash "$R/tools/host_sanitize.sh" tsan-run \
         || exit $? ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac

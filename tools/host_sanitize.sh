@@ -33,6 +33,9 @@ build)
     -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/mine_chain"
   $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g $SAN -pthread -I "$R/include" "$R/examples/board_two_ctx.c" \
     -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/board_two_ctx"
+  # round 6: pow_group_init's deadline (non-blocking init, abort of a communicator still initialising)
+  $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g $SAN -I "$R/include" "$R/examples/group_init_deadline.c" \
+    -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$O/group_init_deadline"
   # the test build of the node (-DPOW_NODE_TEST_KNOBS): the runs below use its race-shaping switches
   $CLANGXX -std=c++17 -O1 -g $SAN -pthread -DPOW_NODE_TEST_KNOBS -I "$R/include" -I "$MPI_INC" \
     "$R/mpi_blockchain_amd/csrc/node/pow_node.cpp" -L "$O" -lpow_gpu -Wl,-rpath,'$ORIGIN' \
@@ -46,6 +49,8 @@ run)
   export LD_LIBRARY_PATH="$O${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}"
   "$O/mine_chain" 10 12
   POW_GRID_PER_CU=4 "$O/board_two_ctx"
+  POW_TEST_RCCL_LIB="$R/tests/stub_rccl/libstub_rccl.so" "$O/group_init_deadline" 3000
+  "$O/group_init_deadline" 3000
   W=$(mktemp -d)
   cd "$W"
   export LD_LIBRARY_PATH="/lib/x86_64-linux-gnu:$MPI_LIB:$LD_LIBRARY_PATH"
@@ -89,6 +94,8 @@ tsan-build)
     -Wl,-rpath,'$ORIGIN' "$MPI_LIB/libmpi.so" -Wl,-rpath-link,"$MPI_LIB" -o "$T/pow_node_tsan"
   $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g -fsanitize=thread -pthread -I "$R/include" \
     "$R/examples/board_two_ctx.c" -L "$T" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$T/board_two_ctx_tsan"
+  $CLANG -std=c11 -D_POSIX_C_SOURCE=200809L -O1 -g -fsanitize=thread -pthread -I "$R/include" \
+    "$R/examples/group_init_deadline.c" -L "$T" -lpow_gpu -Wl,-rpath,'$ORIGIN' -o "$T/group_init_deadline_tsan"
   echo "built $T"
   ;;
 tsan-run)
@@ -100,6 +107,10 @@ tsan-run)
   export TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1:suppressions=$S"
   export LD_LIBRARY_PATH="/lib/x86_64-linux-gnu:$MPI_LIB${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}"
   POW_GRID_PER_CU=4 "$T/board_two_ctx_tsan"
+  # RCCL's own threads are not instrumented either (the bootstrap and proxy threads of the real-RCCL run)
+  echo "called_from_lib:librccl.so" >> "$S"
+  POW_TEST_RCCL_LIB="$R/tests/stub_rccl/libstub_rccl.so" "$T/group_init_deadline_tsan" 3000
+  "$T/group_init_deadline_tsan" 3000
   W=$(mktemp -d)
   cd "$W"
   /opt/conda/bin/mpiexec -np 4 "$T/pow_node_tsan" --difficulty 9
