@@ -3,7 +3,7 @@
  * group whose rank 1 never calls pow_group_init (a rank that died during GPU
  * set-up, say).  The reference would wait forever, as its ranks do in
  * MPI_Recv (node.cpp:155-161); pow_group_init must instead return POW_ECOMM
- * once its deadline passes (POW_GROUP_INIT_TIMEOUT_MS), with the rank, the
+ * once its deadline passes (pow_group_init_within's timeout), with the rank, the
  * group size, the device and the time waited in pow_last_error(), and leave
  * the context usable: a one-rank group on it then forms, all-reduces and mines
  * S0 at d = 21 to its lowest solving counter, 2392323
@@ -36,9 +36,6 @@ static int fail(const char* what) {
 
 int main(int argc, char** argv) {
   const long ms = argc > 1 ? atol(argv[1]) : 3000;
-  char env[32];
-  snprintf(env, sizeof env, "%ld", ms);
-  setenv("POW_GROUP_INIT_TIMEOUT_MS", env, 1);
   pow_ctx* ctx = NULL;
   if (pow_init(0, &ctx) != POW_OK) return fail("pow_init");
 
@@ -46,7 +43,7 @@ int main(int argc, char** argv) {
   if (pow_group_unique_id(id) != POW_OK) return fail("pow_group_unique_id");
   pow_group* g = NULL;
   const double t0 = now_s();
-  const int rc = pow_group_init(ctx, 2, 0, id, &g);
+  const int rc = pow_group_init_within(ctx, 2, 0, id, (unsigned)ms, &g);
   const double dt = now_s() - t0;
   printf("lonely rank 0 of 2: rc %d after %.3f s: %s\n", rc, dt, pow_last_error());
   if (rc != POW_ECOMM || g != NULL) return fail("expected POW_ECOMM and no group");

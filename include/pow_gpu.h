@@ -268,12 +268,14 @@ int pow_group_unique_id(uint8_t id[POW_GROUP_ID_BYTES]);
 /* Joins the RCCL communicator on ctx's GPU; returns once all ranks joined.
  * Bounded: the communicator is made non-blocking (ncclCommInitRankConfig,
  * config.blocking = 0) and polled (ncclCommGetAsyncError) until every rank
- * joined or 60 s (POW_GROUP_INIT_TIMEOUT_MS) passed; then it is aborted
- * (ncclCommAbort) and POW_ECOMM names the rank, nranks, device and elapsed
- * time.  (The reference's ranks block in MPI_Recv with no bound,
- * node.cpp:155-161.) */
+ * joined or 60 s passed; then it is aborted (ncclCommAbort) and POW_ECOMM
+ * names the rank, nranks, device and elapsed time.  (The reference's ranks
+ * block in MPI_Recv with no bound, node.cpp:155-161.) */
 int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
                    pow_group** out);
+/* pow_group_init with the caller's deadline for every rank to join (ms, > 0). */
+int pow_group_init_within(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
+                          unsigned timeout_ms, pow_group** out);
 /* The same group over a reduction the caller supplies instead of RCCL: the
  * rounds, the stop board and the {counter, go, ok} consensus of
  * pow_group_mine[_any] are unchanged, only the one all-reduce per round goes

@@ -137,6 +137,8 @@ def load(test_hooks: bool = False) -> ctypes.CDLL:
         "pow_group_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "pow_group_init": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                             ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "pow_group_init_within": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint,
+                                   ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "pow_group_init_custom": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, REDUCE_FN, ctypes.c_void_p,
                                    ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "pow_group_destroy": ([ctypes.c_void_p], None),
@@ -171,6 +173,7 @@ EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_las
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
            "pow_dev_read", "pow_valu_peak", "pow_valu_rate", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
+           "pow_group_init_within",
            "pow_group_init_custom", "pow_group_destroy", "pow_group_info", "pow_group_rccl_path", "pow_group_last_search",
            "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",
            "pow_board_open", "pow_board_unlink", "pow_board_close", "pow_board_bind", "pow_board_post",

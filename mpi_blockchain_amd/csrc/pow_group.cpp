@@ -142,13 +142,8 @@ uint64_t now_ns() {
   return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
 }
 
-// pow_group_init's deadline for every rank to join the communicator: 60 s, or
-// POW_GROUP_INIT_TIMEOUT_MS.
-uint64_t init_timeout_ns() {
-  if (const char* e = getenv("POW_GROUP_INIT_TIMEOUT_MS"))
-    if (const unsigned long long ms = strtoull(e, nullptr, 0)) return ms * 1000000ull;
-  return 60ull * 1000000000ull;
-}
+// pow_group_init's deadline for every rank to join the communicator.
+constexpr unsigned kInitTimeoutMs = 60000;
 
 // The communicator is non-blocking (config.blocking = 0): RCCL calls on it may
 // return ncclInProgress while their work goes on in the background (joining
@@ -412,10 +407,16 @@ int pow_group_unique_id(uint8_t id[POW_GROUP_ID_BYTES]) {
 
 int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
                    pow_group** out) {
+  return pow_group_init_within(ctx, nranks, rank, id, kInitTimeoutMs, out);
+}
+
+int pow_group_init_within(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROUP_ID_BYTES],
+                          unsigned timeout_ms, pow_group** out) {
   if (!out) return pow_set_error(POW_EINVAL, "null out");
   *out = nullptr;
   if (!ctx || !id) return pow_set_error(POW_EINVAL, "null ctx/id");
   if (nranks < 1 || rank < 0 || rank >= nranks) return pow_set_error(POW_EINVAL, "bad rank/nranks");
+  if (timeout_ms == 0) return pow_set_error(POW_EINVAL, "timeout_ms = 0");
   const Rccl& R = rccl();
   if (R.why[0]) return pow_set_error(POW_ECOMM, R.why);
   hipError_t e = hipSetDevice(pow_ctx_device(ctx));
@@ -441,11 +442,11 @@ int pow_group_init(pow_ctx* ctx, int nranks, int rank, const uint8_t id[POW_GROU
   // Non-blocking init under a deadline: ncclCommInitRank would wait for every
   // rank with no bound, so one rank that fails before it joins (a GPU set-up
   // error, a wrong device map, an exception) would hang the other N - 1
-  // forever.  Here they give up after init_timeout_ns(), abort the
-  // half-built communicator and report who waited for how long.
+  // forever.  Here they give up after timeout_ms, abort the half-built
+  // communicator and report who waited for how long.
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   cfg.blocking = 0;
-  const uint64_t t0 = now_ns(), budget = init_timeout_ns();
+  const uint64_t t0 = now_ns(), budget = (uint64_t)timeout_ms * 1000000ull;
   ncclResult_t r = R.comm_init_rank_config(&g->comm, nranks, u, rank, &cfg);
   bool late = false;
   if ((r == ncclSuccess || r == ncclInProgress) && g->comm) r = comm_settle(g->comm, t0 + budget, &late);

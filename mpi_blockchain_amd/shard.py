@@ -124,7 +124,9 @@ class RcclGroup(_Group):
     a C/C++ caller — the reference's node is C++ — uses; ranks exchange the
     128-byte RCCL id by any means (``from_torch`` uses torch.distributed)."""
 
-    def __init__(self, miner, rank: int, world: int, unique_id: bytes):
+    def __init__(self, miner, rank: int, world: int, unique_id: bytes, timeout_ms: int | None = None):
+        """Joins the communicator; raises PowError (POW_ECOMM) if not every
+        rank joined within `timeout_ms` (default: pow_group_init's 60 s)."""
         from ._lib import GROUP_ID_BYTES
 
         if len(unique_id) != GROUP_ID_BYTES:
@@ -132,7 +134,11 @@ class RcclGroup(_Group):
         self.miner, self.rank, self.world = miner, rank, world
         self.L = miner.L
         self.g = ctypes.c_void_p()
-        check(miner.L.pow_group_init(miner.ctx, world, rank, unique_id, ctypes.byref(self.g)), miner.L)
+        if timeout_ms is None:
+            rc = miner.L.pow_group_init(miner.ctx, world, rank, unique_id, ctypes.byref(self.g))
+        else:
+            rc = miner.L.pow_group_init_within(miner.ctx, world, rank, unique_id, timeout_ms, ctypes.byref(self.g))
+        check(rc, miner.L)
 
     @staticmethod
     def make_unique_id(L: ctypes.CDLL | None = None) -> bytes:
