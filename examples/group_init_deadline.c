@@ -36,8 +36,10 @@ static int fail(const char* what) {
 
 int main(int argc, char** argv) {
   const long ms = argc > 1 ? atol(argv[1]) : 3000;
+  setvbuf(stdout, NULL, _IONBF, 0);  /* every line out at once: a run killed by its time limit still shows its stage */
   pow_ctx* ctx = NULL;
   if (pow_init(0, &ctx) != POW_OK) return fail("pow_init");
+  printf("stage: joining a 2-rank group alone (deadline %ld ms)\n", ms);
 
   uint8_t id[POW_GROUP_ID_BYTES];
   if (pow_group_unique_id(id) != POW_OK) return fail("pow_group_unique_id");
@@ -52,6 +54,7 @@ int main(int argc, char** argv) {
     return fail("error text");
 
   /* the context is still good: a one-rank group forms, all-reduces and mines */
+  printf("stage: one-rank group\n");
   if (pow_group_unique_id(id) != POW_OK) return fail("pow_group_unique_id (2)");
   if (pow_group_init(ctx, 1, 0, id, &g) != POW_OK) return fail("pow_group_init (1 rank)");
   uint64_t v[2] = {5, 7};
@@ -70,6 +73,7 @@ int main(int argc, char** argv) {
     return fail("pow_group_last_search");
   printf("one-rank group: counter %llu, %u rounds, board %d/%d, mine %.3f ms, all-reduce %.3f ms\n",
          (unsigned long long)ctr, info.rounds, info.board_open, info.board_bound, info.mine_ms, info.allreduce_ms);
+  printf("stage: destroy\n");
   pow_group_destroy(g);
   pow_destroy(ctx);
   printf("ok\n");

@@ -242,10 +242,13 @@ struct pow_ctx {
   // latency launch, and of a throughput launch on top of its per-counter share.
   uint64_t watchdog_ns = 10ull * 1000000000ull;
   // A watchdog fired (or a direct dispatch was refused after its packet slot
-  // was reserved): a launch of this context may still be queued and write its
-  // buffers, whatever the launch path.  pow_destroy then leaks them, and
-  // pow_group_* do not queue a collective behind the stuck launch.
+  // was reserved): a launch of this context may still be queued.  pow_group_*
+  // then do not queue a collective behind it; pow_destroy frees only what a
+  // bounded wait shows drained.
   bool wedged = false;
+#ifdef POW_TEST_HOOKS
+  bool aql_lost = false;  // the direct dispatcher was closed with a packet still in flight
+#endif
   pow_stats stats{};
 };
 
@@ -477,7 +480,7 @@ bool aql_usable(pow_ctx* ctx) {
   if (!ctx->aql) return false;
   if (pow_aql_status(ctx->aql) >= 0) return true;
   ctx->aql_why = "the dispatch queue reported an error; back on the HIP launch path";
-  if (!pow_aql_close(ctx->aql)) ctx->wedged = true;  // a packet may still be in flight
+  if (!pow_aql_close(ctx->aql)) ctx->wedged = ctx->aql_lost = true;  // a packet may still be in flight
   ctx->aql = nullptr;
   return false;
 }
@@ -763,16 +766,19 @@ int pow_init(int device, pow_ctx** out) {
 void pow_destroy(pow_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  // A context whose launch never completed (a watchdog error, on either launch
-  // path: direct-dispatch packets are not on the stream, so a stream wait
-  // would not see them) is left allocated rather than freed under a kernel
-  // that may still write it.  Otherwise the wait is bounded too (the base
-  // deadline + 10 s).  (No event: pow_init failed before any launch, nothing
-  // is queued.)
-  if (ctx->wedged) return;
+  // A context whose launch has not completed (after a watchdog error) is left
+  // allocated rather than freed under a kernel that may still write it.  Each
+  // launch path has its own bounded wait: the stream (the base deadline +
+  // 10 s; a launch the watchdog only stopped waiting for usually ends within
+  // it, and its stream, and with it the hardware queue, are then released:
+  // leaking every wedged context's stream instead put 4 more queues on the
+  // test process and starved an 8-rank network), and for
+  // direct-dispatch packets, which the stream does not see, the dispatcher's
+  // completion signal (pow_aql_close).  (No event: pow_init failed before any
+  // launch, nothing is queued.)
   if (ctx->stream && ctx->ev_block && stream_wait_for(ctx, "pow_destroy", 10ull * 1000000000ull) != POW_OK) return;
 #ifdef POW_TEST_HOOKS
-  if (!pow_aql_close(ctx->aql)) return;  // its last packet did not complete: keep what it may write
+  if (ctx->aql_lost || !pow_aql_close(ctx->aql)) return;  // a packet may still write: keep what it writes
 #endif
   (void)hipFree(ctx->d_blob);
   if (ctx->h_blob) (void)hipHostFree(ctx->h_blob);

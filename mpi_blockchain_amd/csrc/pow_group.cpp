@@ -33,10 +33,14 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <thread>
 
 #include "../../include/pow_gpu.h"
 #include "pow_template.h"
@@ -166,6 +170,56 @@ ncclResult_t comm_settle(ncclComm_t c, uint64_t deadline_ns, bool* late) {
     const timespec nap{0, 200000};  // 0.2 ms: a peer that is late by seconds costs no spinning core
     nanosleep(&nap, nullptr);
   }
+}
+
+// ncclCommAbort with a bound.  RCCL 2.27.7's abort of a communicator whose
+// init is still waiting for a missing peer did not return in 37 s on the
+// MI355X box: the init thread kept spinning in the bootstrap, and the abort
+// waits for it (profiles/r06/verify/rccl_abort_probe).  So the abort runs on a
+// detached thread and is given `grace_ms`; past that the communicator (and the
+// thread) are left behind, and the caller, whose rank has already failed,
+// goes on.  true = the abort returned in time.
+bool abort_bounded(ncclComm_t c, unsigned grace_ms) {
+  auto done = std::make_shared<std::atomic<bool>>(false);
+  std::thread([c, done] {
+    (void)rccl().comm_abort(c);
+    done->store(true, std::memory_order_release);
+  }).detach();
+  const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(grace_ms);
+  while (!done->load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until)
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  return done->load(std::memory_order_acquire);
+}
+
+constexpr unsigned kAbortGraceMs = 5000;
+
+// One ncclCommInitRankConfig call, run on a helper thread so that the caller
+// can stop waiting for it.  RCCL 2.27.7 does not return from the call until
+// the communicator is complete even with config.blocking = 0 (1 rank: 5.5 s,
+// ncclSuccess; 2 ranks with the peer missing: no return in 40 s; its own init
+// thread does the work while the calling thread sleeps in a wait loop,
+// profiles/r06/verify/rccl_abort_probe).  A caller that gives up marks the
+// job abandoned; should the call still return later, the helper aborts the
+// communicator nobody will use.
+struct InitJob {
+  std::atomic<int> state{0};  // 0 running, 1 returned, 2 abandoned by the caller
+  ncclComm_t comm = nullptr;
+  ncclResult_t r = ncclInternalError;
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  ncclUniqueId id{};
+  int nranks = 0, rank = 0, device = 0;
+};
+
+void run_init(std::shared_ptr<InitJob> job) {
+  ncclComm_t c = nullptr;
+  ncclResult_t r = ncclUnhandledCudaError;
+  if (hipSetDevice(job->device) == hipSuccess)  // RCCL binds the communicator to the calling thread's device
+    r = rccl().comm_init_rank_config(&c, job->nranks, job->id, job->rank, &job->cfg);
+  job->comm = c;
+  job->r = r;
+  int running = 0;
+  if (!job->state.compare_exchange_strong(running, 1, std::memory_order_acq_rel) && c)
+    (void)rccl().comm_abort(c);  // abandoned: nobody will use this communicator
 }
 
 }  // namespace
@@ -439,30 +493,58 @@ int pow_group_init_within(pow_ctx* ctx, int nranks, int rank, const uint8_t id[P
   if (nranks <= POW_BOARD_MAX_SLOTS && pow_board_open(name, nranks, &g->board) != POW_OK) g->board = nullptr;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
-  // Non-blocking init under a deadline: ncclCommInitRank would wait for every
-  // rank with no bound, so one rank that fails before it joins (a GPU set-up
-  // error, a wrong device map, an exception) would hang the other N - 1
-  // forever.  Here they give up after timeout_ms, abort the half-built
-  // communicator and report who waited for how long.
-  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;
+  // Init under a deadline: ncclCommInitRank would wait for every rank with
+  // no bound, so one rank that fails before it joins (a GPU set-up error, a
+  // wrong device map, an exception) would hang the other N - 1 forever.  Here
+  // they give up after timeout_ms and report who waited for how long.  The
+  // call runs on a helper thread (InitJob: RCCL may block in it whatever the
+  // config says), with a non-blocking config (an RCCL that honours it returns
+  // ncclInProgress at once; the state is then polled and the half-built
+  // communicator aborted at the deadline).
+  auto job = std::make_shared<InitJob>();
+  job->cfg.blocking = 0;
+  job->id = u;
+  job->nranks = nranks;
+  job->rank = rank;
+  job->device = pow_ctx_device(ctx);
   const uint64_t t0 = now_ns(), budget = (uint64_t)timeout_ms * 1000000ull;
-  ncclResult_t r = R.comm_init_rank_config(&g->comm, nranks, u, rank, &cfg);
+  std::thread(run_init, job).detach();
   bool late = false;
+  while (job->state.load(std::memory_order_acquire) == 0 && !late) {
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    late = now_ns() > t0 + budget;
+  }
+  int running = 0;
+  if (late && job->state.compare_exchange_strong(running, 2, std::memory_order_acq_rel)) {
+    pow_board_unlink(name);
+    char buf[480];
+    snprintf(buf, sizeof buf,
+             "ncclCommInitRankConfig: rank %d of %d on HIP device %d: not every rank joined within %.3f s "
+             "(elapsed %.3f s); the call is left to a helper thread, which aborts the communicator if it ever "
+             "returns",
+             rank, nranks, pow_ctx_device(ctx), budget * 1e-9, (now_ns() - t0) * 1e-9);
+    pow_group_destroy(g);
+    return pow_set_error(POW_ECOMM, buf);
+  }
+  late = false;
+  g->comm = job->comm;
+  ncclResult_t r = job->r;
   if ((r == ncclSuccess || r == ncclInProgress) && g->comm) r = comm_settle(g->comm, t0 + budget, &late);
   pow_board_unlink(name);
   if (r != ncclSuccess) {
-    char buf[400];
+    char buf[480];
     const double el = (now_ns() - t0) * 1e-9;
+    const bool aborted = !g->comm || abort_bounded(g->comm, kAbortGraceMs);
+    const char* how = aborted ? "communicator aborted"
+                              : "ncclCommAbort did not return within 5 s: communicator left behind";
     if (late)
       snprintf(buf, sizeof buf,
                "ncclCommInitRankConfig: rank %d of %d on HIP device %d: not every rank joined within %.3f s "
-               "(elapsed %.3f s); communicator aborted",
-               rank, nranks, pow_ctx_device(ctx), budget * 1e-9, el);
+               "(elapsed %.3f s); %s",
+               rank, nranks, pow_ctx_device(ctx), budget * 1e-9, el, how);
     else
-      snprintf(buf, sizeof buf, "ncclCommInitRankConfig: rank %d of %d on HIP device %d: %s (after %.3f s)", rank,
-               nranks, pow_ctx_device(ctx), R.error_string(r), el);
-    if (g->comm) (void)R.comm_abort(g->comm);
+      snprintf(buf, sizeof buf, "ncclCommInitRankConfig: rank %d of %d on HIP device %d: %s (after %.3f s); %s",
+               rank, nranks, pow_ctx_device(ctx), R.error_string(r), el, how);
     g->comm = nullptr;
     pow_group_destroy(g);
     return pow_set_error(POW_ECOMM, buf);
@@ -507,14 +589,19 @@ void pow_group_destroy(pow_group* g) {
     (void)hipSetDevice(pow_ctx_device(g->ctx));
     pow_board_bind(g->ctx, nullptr, 0, 0);
   }
-  if (g->comm) (void)(g->broken ? rccl().comm_abort(g->comm) : rccl().comm_destroy(g->comm));
+  if (g->comm) {
+    if (g->broken)
+      (void)abort_bounded(g->comm, kAbortGraceMs);
+    else
+      (void)rccl().comm_destroy(g->comm);
+  }
   pow_board_close(g->board);
   // hipFree waits for the whole device: after a failed collective (or a stuck
   // launch of the ctx) free the staging buffers only once a bounded wait saw
   // the ctx's stream drain, and leak them otherwise, as pow_destroy does.
   bool drained = true;
   if (g->ctx && (g->d_buf || g->h_buf) && (g->broken || pow_ctx_wedged(g->ctx)))
-    drained = !pow_ctx_wedged(g->ctx) && pow_ctx_stream_wait(g->ctx, "pow_group_destroy", 0) == POW_OK;
+    drained = pow_ctx_stream_wait(g->ctx, "pow_group_destroy", 0) == POW_OK;
   if (drained) {
     if (g->d_buf) (void)hipFree(g->d_buf);
     if (g->h_buf) (void)hipHostFree(g->h_buf);

@@ -174,7 +174,7 @@ def test_bench_eight_rank_rehearsal():
 def test_bench_rank_dies_at_group_init():
     """The first N > 1 contact, broken on purpose: rank 1 of 2 dies after its
     GPU set-up, as the group forms (BENCH_TEST_FAIL).  Rank 0, waiting for it
-    there, is stopped by torch.distributed.run; both ranks leave their
+    there, fails or is stopped by torch.distributed.run; both ranks leave their
     `bench_rank_failure` line naming the phase, no result line is printed, and
     the job ends non-zero in seconds, not at the driver's 600 s limit."""
     import socket
@@ -200,6 +200,8 @@ def test_bench_rank_dies_at_group_init():
     assert sorted(fails) == [0, 1], p.stderr[-3000:]
     assert fails[1]["phase"] == "group_init" and fails[1]["exit_code"] == 6, fails[1]
     assert [x[0] for x in fails[1]["phases_done"]] == ["import", "process_group", "device_init"], fails[1]
-    assert fails[0]["phase"] == "group_init" and fails[0]["exit_code"] == 143, fails[0]
+    # rank 0 waits in the group's id broadcast: gloo sees its peer's socket close (exit 6, the
+    # collective's error) or torch.distributed.run stops it first (SIGTERM, exit 143)
+    assert fails[0]["phase"] == "group_init" and fails[0]["exit_code"] in (6, 143), fails[0]
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
     assert wall < 150, wall
