@@ -69,13 +69,14 @@ class RankPhases:
     writes from whichever thread the signal lands on."""
 
     DEADLINE_S = 570.0
+    SIGTERM_REASON = "SIGTERM (the launcher stops the job: another rank failed, or the job was cancelled)"
 
     def __init__(self, rank: int, world: int, local: int):
         self.rank, self.world, self.local = rank, world, local
         self.t0 = time.monotonic()
         self.phase, self.phase_t0, self.budget = "start", self.t0, None
         self.done: list = []
-        self.lock = threading.Lock()
+        self.lock = threading.RLock()  # re-entrant: the SIGTERM handler may run inside enter() on the main thread
         self.emitted = False
         self.deadline = self.t0 + float(os.environ.get("BENCH_DEADLINE_S", self.DEADLINE_S))
         # Tests only: BENCH_TEST_FAIL="<rank>:<phase>" makes that rank raise on
@@ -86,7 +87,10 @@ class RankPhases:
         if threading.current_thread() is threading.main_thread():
             r, w = os.pipe()
             os.set_blocking(w, False)
-            signal.signal(signal.SIGTERM, lambda *_: None)  # acted on by the watcher (wakeup fd)
+            # Whichever sees SIGTERM first writes the line: the watcher (through the
+            # wakeup fd, while the main thread is blocked in C) or this handler (once
+            # the main thread is back in the interpreter, e.g. a sleep the signal cut short).
+            signal.signal(signal.SIGTERM, lambda *_: self.abort(128 + signal.SIGTERM, self.SIGTERM_REASON))
             signal.set_wakeup_fd(w, warn_on_full_buffer=False)
             self._rfd = r
         else:  # pragma: no cover - bench.main() always runs on the main thread
@@ -128,10 +132,14 @@ class RankPhases:
         sys.exit(code)
 
     def abort(self, code: int, reason: str, **extra) -> None:
-        """From the watcher (the main thread may be stuck in C): the line, then
-        _exit without running teardown that could block on a stuck GPU."""
+        """From the watcher (the main thread may be stuck in C) or the SIGTERM
+        handler: the line, then _exit without running teardown that could
+        block on a stuck GPU.  A second caller (the line is out) waits for the
+        first one's _exit."""
         if self._emit(reason, code, **extra):
             os._exit(code)
+        time.sleep(5)
+        os._exit(code)
 
     def _watch(self) -> None:
         import select
@@ -142,8 +150,7 @@ class RankPhases:
                 if ready:
                     sigs = os.read(self._rfd, 64)
                     if signal.SIGTERM in sigs:
-                        self.abort(128 + signal.SIGTERM, "SIGTERM (the launcher stops the job: another rank failed, "
-                                                         "or the job was cancelled)")
+                        self.abort(128 + signal.SIGTERM, self.SIGTERM_REASON)
             else:  # pragma: no cover
                 time.sleep(0.25)
             now = time.monotonic()

@@ -198,12 +198,16 @@ constexpr unsigned kAbortGraceMs = 5000;
 // the communicator is complete even with config.blocking = 0 (1 rank: 5.5 s,
 // ncclSuccess; 2 ranks with the peer missing: no return in 40 s; its own init
 // thread does the work while the calling thread sleeps in a wait loop,
-// profiles/r06/verify/rccl_abort_probe).  A caller that gives up marks the
-// job abandoned; should the call still return later, the helper aborts the
-// communicator nobody will use.
+// profiles/r06/verify/rccl_abort_probe).  An RCCL that honours the
+// non-blocking config returns ncclInProgress at once; the helper then polls
+// ncclCommGetAsyncError itself until the communicator is ready, so the init
+// completes on the thread that started it (RCCL may keep a pending init in
+// that thread's state).  A failed init is aborted on the helper too.  A caller
+// that gives up marks the job abandoned; the helper then aborts whatever it
+// gets.  The caller only reads the published result.
 struct InitJob {
-  std::atomic<int> state{0};  // 0 running, 1 returned, 2 abandoned by the caller
-  ncclComm_t comm = nullptr;
+  std::atomic<int> state{0};  // 0 running, 1 published, 2 abandoned by the caller
+  ncclComm_t comm = nullptr;  // published: a ready communicator, or null
   ncclResult_t r = ncclInternalError;
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   ncclUniqueId id{};
@@ -215,11 +219,18 @@ void run_init(std::shared_ptr<InitJob> job) {
   ncclResult_t r = ncclUnhandledCudaError;
   if (hipSetDevice(job->device) == hipSuccess)  // RCCL binds the communicator to the calling thread's device
     r = rccl().comm_init_rank_config(&c, job->nranks, job->id, job->rank, &job->cfg);
-  job->comm = c;
-  job->r = r;
+  while (r == ncclInProgress && c && job->state.load(std::memory_order_acquire) == 0) {
+    ncclResult_t st = ncclInProgress;
+    if (rccl().get_async_error(c, &st) != ncclSuccess) st = ncclInternalError;
+    r = st;
+    if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  const bool ok = r == ncclSuccess && c;
+  job->comm = ok ? c : nullptr;
+  job->r = ok ? ncclSuccess : (r == ncclSuccess ? ncclInternalError : r);
   int running = 0;
-  if (!job->state.compare_exchange_strong(running, 1, std::memory_order_acq_rel) && c)
-    (void)rccl().comm_abort(c);  // abandoned: nobody will use this communicator
+  const bool published = job->state.compare_exchange_strong(running, 1, std::memory_order_acq_rel);
+  if (c && (!ok || !published)) (void)rccl().comm_abort(c);  // failed, or nobody will use it
 }
 
 }  // namespace
@@ -497,10 +508,8 @@ int pow_group_init_within(pow_ctx* ctx, int nranks, int rank, const uint8_t id[P
   // no bound, so one rank that fails before it joins (a GPU set-up error, a
   // wrong device map, an exception) would hang the other N - 1 forever.  Here
   // they give up after timeout_ms and report who waited for how long.  The
-  // call runs on a helper thread (InitJob: RCCL may block in it whatever the
-  // config says), with a non-blocking config (an RCCL that honours it returns
-  // ncclInProgress at once; the state is then polled and the half-built
-  // communicator aborted at the deadline).
+  // init runs on a helper thread (InitJob: RCCL may block in the call whatever
+  // the config says), with a non-blocking config.
   auto job = std::make_shared<InitJob>();
   job->cfg.blocking = 0;
   job->id = u;
@@ -526,25 +535,14 @@ int pow_group_init_within(pow_ctx* ctx, int nranks, int rank, const uint8_t id[P
     pow_group_destroy(g);
     return pow_set_error(POW_ECOMM, buf);
   }
-  late = false;
   g->comm = job->comm;
-  ncclResult_t r = job->r;
-  if ((r == ncclSuccess || r == ncclInProgress) && g->comm) r = comm_settle(g->comm, t0 + budget, &late);
+  const ncclResult_t r = job->r;
   pow_board_unlink(name);
   if (r != ncclSuccess) {
     char buf[480];
-    const double el = (now_ns() - t0) * 1e-9;
-    const bool aborted = !g->comm || abort_bounded(g->comm, kAbortGraceMs);
-    const char* how = aborted ? "communicator aborted"
-                              : "ncclCommAbort did not return within 5 s: communicator left behind";
-    if (late)
-      snprintf(buf, sizeof buf,
-               "ncclCommInitRankConfig: rank %d of %d on HIP device %d: not every rank joined within %.3f s "
-               "(elapsed %.3f s); %s",
-               rank, nranks, pow_ctx_device(ctx), budget * 1e-9, el, how);
-    else
-      snprintf(buf, sizeof buf, "ncclCommInitRankConfig: rank %d of %d on HIP device %d: %s (after %.3f s); %s",
-               rank, nranks, pow_ctx_device(ctx), R.error_string(r), el, how);
+    snprintf(buf, sizeof buf,
+             "ncclCommInitRankConfig: rank %d of %d on HIP device %d: %s (after %.3f s); communicator aborted", rank,
+             nranks, pow_ctx_device(ctx), R.error_string(r), (now_ns() - t0) * 1e-9);
     g->comm = nullptr;
     pow_group_destroy(g);
     return pow_set_error(POW_ECOMM, buf);
