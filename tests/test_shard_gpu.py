@@ -309,3 +309,48 @@ def test_native_group_beside_torch_rccl():
             assert t.sum().item() == 4
     finally:
         dist.destroy_process_group()
+
+
+LONELY_TORCH_RCCL = r"""
+import sys, time
+sys.path.insert(0, %r)
+import torch  # torch's RCCL (2.26.6 on this image) is the one pow_group binds, as in bench.py
+from mpi_blockchain_amd._lib import PowError
+from mpi_blockchain_amd.block import make_block
+from mpi_blockchain_amd.miner import GpuMiner
+from mpi_blockchain_amd.shard import RcclGroup, rccl_path
+with GpuMiner(0) as m:
+    print("rccl", rccl_path(m.L), flush=True)
+    t = time.monotonic()
+    try:
+        RcclGroup(m, 0, 2, RcclGroup.make_unique_id(m.L), timeout_ms=3000)
+        print("joined?!", flush=True)
+    except PowError as e:
+        print(f"lonely: {time.monotonic() - t:.3f} s: {e}", flush=True)
+    with RcclGroup(m, 0, 1, RcclGroup.make_unique_id(m.L)) as g:
+        assert g.allreduce([5, 7], "min") == [5, 7]
+        r = g.mine(make_block(1, 0, 9, 1700000000, b""), 0, 1 << 32, 21)
+        print("one-rank group counter", r.counter, flush=True)
+print("ok", flush=True)
+"""
+
+
+def test_group_init_deadline_torch_rccl():
+    """pow_group_init's join deadline with torch's own RCCL, the copy bench.py's
+    ranks bind (2.26.6 honours the non-blocking config, unlike /opt/rocm's
+    2.27.7 that tests/test_c_consumer.py::test_group_init_deadline[rccl]
+    covers): rank 0 of a 2-rank group whose peer never joins gets POW_ECOMM
+    after its 3 s deadline, and the same context then forms a one-rank group
+    that mines S0 at d = 21 to its golden lowest counter."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-c", LONELY_TORCH_RCCL % root],
+                       capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout + p.stderr[-3000:]
+    assert "torch/lib/librccl.so" in p.stdout, p.stdout
+    line = next(ln for ln in p.stdout.splitlines() if ln.startswith("lonely: "))
+    assert "POW_ECOMM" in line and "rank 0 of 2" in line and "not every rank joined within 3.000 s" in line, line
+    assert 2.9 < float(line.split()[1]) < 8.0, line
+    assert "one-rank group counter 2392323" in p.stdout and p.stdout.rstrip().endswith("ok"), p.stdout
