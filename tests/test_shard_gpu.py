@@ -354,3 +354,53 @@ def test_group_init_deadline_torch_rccl():
     assert "POW_ECOMM" in line and "rank 0 of 2" in line and "not every rank joined within 3.000 s" in line, line
     assert 2.9 < float(line.split()[1]) < 8.0, line
     assert "one-rank group counter 2392323" in p.stdout and p.stdout.rstrip().endswith("ok"), p.stdout
+
+
+TWO_RANKS_ONE_GPU = r"""
+import os, sys, time
+sys.path.insert(0, %r)
+import torch  # torch's RCCL, as bench.py's ranks bind it
+from mpi_blockchain_amd._lib import PowError
+from mpi_blockchain_amd.miner import GpuMiner
+from mpi_blockchain_amd.shard import RcclGroup
+rank, idf = int(sys.argv[1]), sys.argv[2]
+with GpuMiner(0) as m:
+    if rank == 0:
+        open(idf + ".tmp", "wb").write(RcclGroup.make_unique_id(m.L))
+        os.replace(idf + ".tmp", idf)
+    while not os.path.exists(idf):
+        time.sleep(0.01)
+    uid = open(idf, "rb").read()
+    t = time.monotonic()
+    try:
+        RcclGroup(m, rank, 2, uid, timeout_ms=20000).close()
+        print(f"rank {rank}: joined", flush=True)
+    except PowError as e:
+        print(f"rank {rank}: {time.monotonic() - t:.3f} s: {e}", flush=True)
+"""
+
+
+def test_real_rccl_two_ranks_one_gpu_fail_fast(tmp_path):
+    """Two processes join one real-RCCL group (torch's copy) on the one GPU of
+    the box: RCCL's bootstrap connects them, then RCCL refuses two ranks on one
+    device.  Neither rank hangs: each pow_group_init returns POW_ECOMM, either
+    with RCCL's own error or at its 20 s deadline, and both processes exit 0.
+    This is the only multi-process run of RCCL itself a one-GPU box allows."""
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    idf = str(tmp_path / "id")
+    t = time.monotonic()
+    procs = [subprocess.Popen(["timeout", "-k", "5", "90", sys.executable, "-c", TWO_RANKS_ONE_GPU % root, str(r), idf],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    wall = time.monotonic() - t
+    for r, (p, (out, err)) in enumerate(zip(procs, outs)):
+        print(out.strip())
+        assert p.returncode == 0, (r, out, err[-3000:])
+        line = next(ln for ln in out.splitlines() if ln.startswith(f"rank {r}: "))
+        assert "POW_ECOMM" in line and f"rank {r} of 2 on HIP device 0" in line, line
+        assert float(line.split()[2]) < 26.0, line
+    assert wall < 90, wall
