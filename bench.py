@@ -80,8 +80,13 @@ class RankPhases:
         self.emitted = False
         self.deadline = self.t0 + float(os.environ.get("BENCH_DEADLINE_S", self.DEADLINE_S))
         # Tests only: BENCH_TEST_FAIL="<rank>:<phase>" makes that rank raise on
-        # entering that phase (a rank that dies before the group forms).
+        # entering that phase (a rank that dies before the group forms);
+        # BENCH_TEST_HANG="<rank>:<phase>" makes it block there inside a C call
+        # (a rank stuck in a driver call); BENCH_PHASE_SCALE scales every phase
+        # budget (a hang then fails in seconds).
         self.inject = os.environ.get("BENCH_TEST_FAIL", "")
+        self.hang = os.environ.get("BENCH_TEST_HANG", "")
+        self.scale = float(os.environ.get("BENCH_PHASE_SCALE", "1"))
 
     def start(self) -> "RankPhases":
         if threading.current_thread() is threading.main_thread():
@@ -102,9 +107,14 @@ class RankPhases:
         with self.lock:
             now = time.monotonic()
             self.done.append([self.phase, round(now - self.phase_t0, 3)])
-            self.phase, self.phase_t0, self.budget = name, now, budget_s
+            self.phase, self.phase_t0, self.budget = name, now, budget_s * self.scale
         if self.inject == f"{self.rank}:{name}":
             raise RuntimeError(f"BENCH_TEST_FAIL: injected failure of rank {self.rank} entering {name}")
+        if self.hang == f"{self.rank}:{name}":
+            import ctypes
+
+            while True:  # blocked in C, as in a driver call that never returns
+                ctypes.CDLL(None).sleep(3600)
 
     def record(self, reason: str, code: int, **extra) -> dict:
         now = time.monotonic()

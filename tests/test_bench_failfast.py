@@ -92,3 +92,30 @@ def test_rank_dies_before_the_group_forms():
     assert lines[0]["phase"] == "process_group" and lines[0]["exit_code"] == 143, lines[0]
     assert wall < 150, wall
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+
+
+def test_rank_hangs_before_the_group_forms():
+    """2 ranks; rank 1 blocks inside a C call as it enters init_process_group
+    (a rank stuck in a driver call: it neither dies nor joins).  With the
+    phase budgets scaled down (BENCH_PHASE_SCALE) both ranks fail on their
+    own deadlines — rank 1 where it hangs, rank 0 waiting for it in the
+    rendezvous, or stopped by the launcher once rank 1 is gone — each with its
+    line, and the job ends non-zero in seconds."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, BENCH_REHEARSAL="1", BENCH_TEST_HANG="1:process_group", BENCH_PHASE_SCALE="0.04")
+    t = time.monotonic()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "1", "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=ROOT)
+    wall = time.monotonic() - t
+    assert p.returncode != 0
+    lines = {f["rank"]: f for f in failure_lines(p.stderr)}
+    assert sorted(lines) == [0, 1], p.stderr[-3000:]
+    assert lines[1]["phase"] == "process_group" and lines[1]["exit_code"] == 7 and "budget" in lines[1]["reason"], \
+        lines[1]
+    assert lines[0]["phase"] == "process_group" and lines[0]["exit_code"] in (7, 143), lines[0]
+    assert wall < 60, wall
