@@ -663,7 +663,9 @@ def board_summary(per_rank: list[dict], stop_us: list[float], world: int) -> dic
     search with a finder (the last rank's mine return minus the finder's,
     CLOCK_MONOTONIC on one node).  With a board that is missing or not coherent
     across GPUs the peers only stop at the round's all-reduce, after their
-    whole shard: the latency is then hundreds of ms, not tens of us."""
+    whole shard: the latency is then hundreds of ms, not tens of us.  It is
+    signed: the peers' kernels see the finder's hit on the board as its kernel
+    stores it, so they can return before the finder's own host has seen it."""
     out = {"per_rank": per_rank,
            "all_ranks_board": all(r["board_open"] and r["board_bound_every_search"] for r in per_rank),
            "stop_latency_samples": len(stop_us)}
@@ -675,14 +677,17 @@ def board_summary(per_rank: list[dict], stop_us: list[float], world: int) -> dic
     if stop_us:
         med = statistics.median(stop_us)
         out["stop_latency_us_median"] = round(med, 1)
+        out["stop_latency_us_min"] = round(min(stop_us), 1)
         out["stop_latency_us_max"] = round(max(stop_us), 1)
         out["peers_stopped_by_board"] = out["all_ranks_board"] and med < BOARD_STOP_OK_US
     else:
         out["stop_latency_us_median"] = None
         out["peers_stopped_by_board"] = None
-    out["note"] = ("stop latency = max over ranks of the time each rank's pow_mine_any returned, minus the "
-                   "finder's (CLOCK_MONOTONIC); peers_stopped_by_board needs every rank bound to the board and a "
-                   f"median under {BOARD_STOP_OK_US} us (a peer that runs out its 2^32-counter shard takes ~470 ms)")
+    out["note"] = ("stop latency = when the last peer's pow_mine_any returned (a rank that found nothing) minus "
+                   "when the finder's did (CLOCK_MONOTONIC, one node), per search with both; negative = the peers "
+                   "stopped before the finder's host saw its own hit; peers_stopped_by_board needs every rank bound "
+                   f"to the board and a median under {BOARD_STOP_OK_US} us (a peer that runs out its 2^32-counter "
+                   "shard takes ~470 ms)")
     return out
 
 
@@ -724,10 +729,11 @@ def group_search(group, rank: int, world: int, d: int = 30, n_templates: int = 2
         mine_ms.append(info["mine_ms"])
         ar_ms.append(info["allreduce_ms"])
         rounds.append(info["rounds"])
+        # the finder's return (the first, if several found) and the last peer's (a rank that found nothing)
         fin = group.allreduce([info["mine_end_ns"] if info["local_found"] else U64MAX], "min")[0]
-        last_end = group.allreduce([info["mine_end_ns"]], "max")[0]
-        if fin != U64MAX and world > 1:
-            stop_us.append((last_end - fin) / 1e3)
+        peer_end = group.allreduce([0 if info["local_found"] else info["mine_end_ns"]], "max")[0]
+        if fin != U64MAX and peer_end and world > 1:
+            stop_us.append((peer_end - fin) / 1e3)  # signed: < 0 = the peers stopped before the finder returned
         hashes.append(group.allreduce([r.hashes if r else 0], "sum")[0])
         c = r.counter if r else U64MAX
         counters.append(r.counter if r else None)
@@ -1188,6 +1194,15 @@ def run_rank(args, ph: RankPhases, world: int, rank: int, local: int) -> None:
     if do_proto:
         pids = [None] * world
         dist.all_gather_object(pids, os.getpid())
+    # Every rank releases the library's communicator at the same point, before
+    # rank 0 goes on alone to config 5: RCCL's teardown of a multi-rank
+    # communicator may wait for its peers' (ncclCommFinalize is "globally
+    # quiescent"), so ranks 1..N-1 must not be left waiting in it for rank 0.
+    had_group = group is not None
+    if group is not None and dist is not None:
+        ph.enter("group_close", 60)
+        group.close()
+        group = None
     if rank != 0:
         ph.enter("teardown", 60)
         buf.free()
@@ -1203,11 +1218,11 @@ def run_rank(args, ph: RankPhases, world: int, rank: int, local: int) -> None:
             {"skipped": "bench ranks 1..N-1 did not exit within 120 s"}
     ph.enter("report", 480)
     collective = ("gloo all_reduce(min,sum) per step via pow_group_allreduce_u64 (pow_group_init_custom; "
-                  "rehearsal: ranks share one GPU)" if transport == "gloo" and rehearsal and group is not None else
+                  "rehearsal: ranks share one GPU)" if transport == "gloo" and rehearsal and had_group else
                   "stand-in RCCL (tests/stub_rccl, shared memory) all_reduce(min,sum) per step via "
                   "pow_group_allreduce_u64 (pow_group_init; rehearsal: ranks share one GPU)"
-                  if transport == "rccl_stub" and group is not None else
-                  "rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if group is not None and world > 1
+                  if transport == "rccl_stub" and had_group else
+                  "rccl all_reduce(min,sum) per step via pow_group_allreduce_u64" if had_group and world > 1
                   else f"{dist.get_backend()} all_reduce(min,sum) per step via torch.distributed" if dist is not None
                   else "none (single process)")
 

@@ -318,6 +318,9 @@ def test_board_summary():
     ok_rank = {"board_open": True, "board_bound_every_search": True}
     b = bench.board_summary([dict(ok_rank, rank=r) for r in range(8)], [35.0, 40.0, 80.0], 8)
     assert b["all_ranks_board"] and b["peers_stopped_by_board"] and b["stop_latency_us_median"] == 40.0
+    # signed: peers that stopped before the finder's host returned
+    b = bench.board_summary([dict(ok_rank, rank=r) for r in range(2)], [-12.5, -3.0, 4.0], 2)
+    assert b["peers_stopped_by_board"] and b["stop_latency_us_min"] == -12.5 and b["stop_latency_us_median"] == -3.0
     b = bench.board_summary([dict(ok_rank, rank=0), dict(ok_rank, rank=1, board_open=False)], [30.0], 2)
     assert not b["all_ranks_board"] and b["peers_stopped_by_board"] is False
     b = bench.board_summary([dict(ok_rank, rank=r) for r in range(2)], [460_000.0, 470_000.0], 2)

@@ -7,7 +7,9 @@
 #   tests            the whole GPU suite (pytest -m gpu)
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (default: N = 1, every block of the JSON line)
-#   profile          tools/profile_round.sh r05 (kernel trace + 4 PMC passes of the bench workload)
+#   profile          tools/profile_round.sh r06 (kernel trace + 4 PMC passes of the bench workload)
+#   rehearse N T     bench.py's N > 1 path with N ranks sharing the GPU (BENCH_REHEARSAL=1), transport T
+#                    (gloo | rccl_stub): the JSON line with timing, board and placement blocks
 #   fuzz             randomised parity, shipped library: 1,000 cases (tests/parity_fuzz.py)
 #   fuzz_big         10,000 cases, then 2,000 each on the test library: K1' asm variants
 #                    (POW_LAT_WPS=4), + d > 32 variants, and K1 alone (POW_LAT_MAX=0)
@@ -27,7 +29,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 S="$R/tools/gpu_step.sh"
 L="$R/mpi_blockchain_amd/libpow_gpu.so"
-STEPS=" tests smoke bench profile fuzz fuzz_big soak_mixed queue_pressure queue_ab ab_k1 ab_k2 ttb k2_trace pmc_onewave sanitize "
+STEPS=" tests smoke bench profile rehearse fuzz fuzz_big soak_mixed queue_pressure queue_ab ab_k1 ab_k2 ttb k2_trace pmc_onewave sanitize "
 libs() {  # the library arguments of an A/B step
   LIBS=()
   while [ $# -gt 0 ] && [[ "$STEPS" != *" $1 "* ]]; do LIBS+=("$1"); shift; done
@@ -40,7 +42,11 @@ while [ $# -gt 0 ]; do
              $S gputests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread || exit $? ;;
     smoke) $S smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) $S bench 900 python -u bench.py || exit $? ;;
-    profile) bash "$R/tools/profile_round.sh" r05 || exit $? ;;
+    profile) bash "$R/tools/profile_round.sh" r06 || exit $? ;;
+    rehearse) n=$1; tr=$2; shift 2
+      BENCH_REHEARSAL=1 BENCH_REHEARSAL_TRANSPORT=$tr $S rehearse_${n}_$tr 900 python -u -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$n" \
+        --steps 2 --warmup 1 || exit $? ;;
     fuzz) $S fuzz 900 python -u tests/parity_fuzz.py --cases 1000 --seed 404 || exit $? ;;
     fuzz_big) $S fuzz_big 900 python -u tests/parity_fuzz.py --cases 10000 --seed 4004 &&
       POW_LAT_WPS=4 $S fuzz_lat_asm 900 python -u tests/parity_fuzz.py --test-hooks --cases 2000 --seed 4005 &&
