@@ -172,13 +172,15 @@ ncclResult_t comm_settle(ncclComm_t c, uint64_t deadline_ns, bool* late) {
   }
 }
 
-// ncclCommAbort with a bound.  RCCL 2.27.7's abort of a communicator whose
-// init is still waiting for a missing peer did not return in 37 s on the
-// MI355X box: the init thread kept spinning in the bootstrap, and the abort
-// waits for it (profiles/r06/verify/rccl_abort_probe).  So the abort runs on a
-// detached thread and is given `grace_ms`; past that the communicator (and the
-// thread) are left behind, and the caller, whose rank has already failed,
-// goes on.  true = the abort returned in time.
+// ncclCommAbort with a bound, for a communicator whose collective failed or
+// ran out of time (a peer that never joined it).  RCCL's abort waits for its
+// own threads (the init thread, the proxy), and one of them may be waiting for
+// that peer: on the MI355X box RCCL 2.27.7's init thread spun in the
+// bootstrap for as long as the missing peer stayed away
+// (profiles/r06/verify/rccl_abort_probe).  So the abort runs on a detached
+// thread and is given `grace_ms`; past that the communicator (and the thread)
+// are left behind, and the caller, whose rank has already failed, goes on.
+// true = the abort returned in time.
 bool abort_bounded(ncclComm_t c, unsigned grace_ms) {
   auto done = std::make_shared<std::atomic<bool>>(false);
   std::thread([c, done] {
