@@ -404,3 +404,96 @@ def test_real_rccl_two_ranks_one_gpu_fail_fast(tmp_path):
         assert "POW_ECOMM" in line and f"rank {r} of 2 on HIP device 0" in line, line
         assert float(line.split()[2]) < 26.0, line
     assert wall < 90, wall
+
+
+BROKEN_GROUP = r"""
+import os, sys, time
+sys.path.insert(0, %r)
+rank, idf, case, stub = int(sys.argv[1]), sys.argv[2], sys.argv[3], sys.argv[4]
+os.environ.update(POW_TEST_RCCL_LIB=stub, POW_STUB_TIMEOUT_S="3")
+if case == "wedged" and rank == 1:  # this rank's launches stall 300 ms behind a 30 ms watchdog
+    os.environ.update(POW_TEST_STALL_US="300000", POW_WATCHDOG_MS="30")
+from mpi_blockchain_amd._lib import PowError
+from mpi_blockchain_amd.block import make_block
+from mpi_blockchain_amd.miner import GpuMiner
+from mpi_blockchain_amd.shard import RcclGroup
+S0 = make_block(1, 0, 9, 1700000000, b"")
+m = GpuMiner(0, test_hooks=True)
+if rank == 0:
+    open(idf + ".tmp", "wb").write(RcclGroup.make_unique_id(m.L))
+    os.replace(idf + ".tmp", idf)
+while not os.path.exists(idf):
+    time.sleep(0.01)
+g = RcclGroup(m, rank, 2, open(idf, "rb").read(), timeout_ms=30000)
+print(f"rank {rank}: joined", flush=True)
+if case == "exits" and rank == 1:
+    os._exit(0)  # dies once the group has formed
+t = time.monotonic()
+try:
+    # d = 21: the first launch of each shard is the latency kernel K1', whose watchdog (30 ms +
+    # 2 ns per counter) the wedged rank's 300 ms stall outlasts; rank 0 finds S0's 2392323 at once
+    r = g.mine(S0, 0, 1 << 40, 21, any_solution=True)
+    print(f"rank {rank}: mined?! {r}", flush=True)
+except PowError as e:
+    print(f"rank {rank}: mine failed after {time.monotonic() - t:.3f} s: {e}", flush=True)
+try:
+    g.allreduce([1], "sum")
+    print(f"rank {rank}: allreduce ok?!", flush=True)
+except PowError as e:
+    print(f"rank {rank}: allreduce after: {e}", flush=True)
+t = time.monotonic()
+g.close()
+print(f"rank {rank}: close {time.monotonic() - t:.3f} s", flush=True)
+if not (case == "wedged" and rank == 1):  # a context whose watchdog fired is not reused
+    print(f"rank {rank}: after {m.mine(S0, 0, 1 << 32, 21).counter}", flush=True)
+m.close()
+print(f"rank {rank}: ok", flush=True)
+"""
+
+
+def _field(out: str, rank: int, key: str) -> str:
+    return next(ln for ln in out.splitlines() if ln.startswith(f"rank {rank}: {key}"))
+
+
+@pytest.mark.parametrize("case", ["exits", "wedged"])
+def test_group_broken_fails_every_rank_fast(tmp_path, case):
+    """A group whose round cannot complete, through pow_group_init's
+    RCCL leg with the stand-in (its barrier gives up after 3 s here, as a
+    stand-in for pow_group's own deadline on RCCL's asynchronous all-reduce):
+      exits  - rank 1 dies once the group has formed: rank 0's round-end
+               all-reduce fails (POW_ECOMM);
+      wedged - rank 1's launch is stuck (its watchdog fires): rank 1 returns
+               its own error at once without joining the round's all-reduce,
+               and rank 0's all-reduce fails at the stand-in's deadline.
+    Every later collective of a broken group returns POW_ECOMM at once,
+    pow_group_destroy returns (bounded drain), and a healthy context mines
+    S0 at d = 21 to 2392323 afterwards."""
+    import subprocess
+    import sys
+
+    from mpi_blockchain_amd.build import STUB_LIB, build_test_stub
+
+    build_test_stub()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    idf = str(tmp_path / "id")
+    procs = [subprocess.Popen(["timeout", "-k", "5", "120", sys.executable, "-c", BROKEN_GROUP % root, str(r), idf,
+                               case, STUB_LIB], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(2)]
+    outs = [p.communicate(timeout=150) for p in procs]
+    for p, (out, err) in zip(procs, outs):
+        print(out.strip())
+        assert p.returncode == 0, (out, err[-3000:])
+    out0, out1 = outs[0][0], outs[1][0]
+    m0 = _field(out0, 0, "mine failed after")
+    assert "POW_ECOMM" in m0 and "ncclAllReduce" in m0 and float(m0.split()[5]) < 15, m0
+    assert "the group is broken" in _field(out0, 0, "allreduce after")
+    assert float(_field(out0, 0, "close").split()[3]) < 10
+    assert _field(out0, 0, "after") == "rank 0: after 2392323" and "rank 0: ok" in out0
+    if case == "exits":
+        assert "rank 1: joined" in out1 and "rank 1: mine" not in out1
+    else:
+        m1 = _field(out1, 1, "mine failed after")
+        assert "POW_EHIP" in m1 and "watchdog" in m1 and "did not join the round's all-reduce" in m1, m1
+        assert float(m1.split()[5]) < 5, m1  # at once: not after the stand-in's 3 s or a round's shard
+        assert "the group is broken" in _field(out1, 1, "allreduce after")
+        assert float(_field(out1, 1, "close").split()[3]) < 15 and "rank 1: ok" in out1
