@@ -137,9 +137,12 @@ class RankPhases:
         return True
 
     def fail(self, code: int, reason: str, **extra) -> None:
-        """A failure the main thread found: the line, then exit `code`."""
+        """A failure the main thread found: the line, then exit `code` at once
+        (os._exit: no atexit teardown of torch's process group or RCCL, which
+        could wait for the very peer that failed)."""
         self._emit(reason, code, **extra)
-        sys.exit(code)
+        sys.stdout.flush()
+        os._exit(code)
 
     def abort(self, code: int, reason: str, **extra) -> None:
         """From the watcher (the main thread may be stuck in C) or the SIGTERM
@@ -1049,8 +1052,8 @@ def run_rank(args, ph: RankPhases, world: int, rank: int, local: int) -> None:
     miner = GpuMiner(local, test_hooks=transport == "rccl_stub")
     # The library's own RCCL communicator (the id travels over torch.distributed);
     # at N = 1 a one-rank group, used only by the group_search measurement.
-    # pow_group_init gives up after 60 s if a peer never joins (non-blocking
-    # ncclCommInitRankConfig under a deadline).
+    # pow_group_init gives up after 60 s if a peer never joins (RCCL's init on
+    # a helper thread under a deadline).
     ph.enter("group_init", 120)
     group, group_err = None, None
     if transport == "gloo":

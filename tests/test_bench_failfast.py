@@ -115,7 +115,8 @@ def test_rank_hangs_before_the_group_forms():
     assert p.returncode != 0
     lines = {f["rank"]: f for f in failure_lines(p.stderr)}
     assert sorted(lines) == [0, 1], p.stderr[-3000:]
-    assert lines[1]["phase"] == "process_group" and lines[1]["exit_code"] == 7 and "budget" in lines[1]["reason"], \
-        lines[1]
-    assert lines[0]["phase"] == "process_group" and lines[0]["exit_code"] in (7, 143), lines[0]
+    # whichever rank's budget runs out first exits 7; the launcher then stops the other (143),
+    # unless its own budget fired too
+    assert all(f["phase"] == "process_group" and f["exit_code"] in (7, 143) for f in lines.values()), lines
+    assert any(f["exit_code"] == 7 and "budget" in f["reason"] for f in lines.values()), lines
     assert wall < 60, wall
