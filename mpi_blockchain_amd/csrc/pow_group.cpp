@@ -332,16 +332,31 @@ struct StatSum {
   }
 };
 
-// The winner's block: nonce + block_hash through a one-counter pow_mine at
-// difficulty 0 (one latency-kernel dispatch that records the digest; the
-// board is unbound by then, so the peers' published hits do not stop it).
-int winner_block(pow_group* g, const pow_block* tmpl, uint64_t ctr, pow_block* out, StatSum& st) {
-  uint64_t c = 0;
-  const int rc = pow_mine(g->ctx, tmpl, ctr, 1, 0, nullptr, 0, out, &c, nullptr);
-  st.add(g->ctx);
-  if (rc < 0) return rc;
-  if (rc != 1 || c != ctr) return pow_set_error(POW_EHIP, "winner re-hash failed");
-  return POW_OK;
+// The winner's digest travels from the rank that found it: its 64-char hex
+// (pow_mine's block_hash) as 4 big-endian words.  false = not 64 hex digits.
+bool digest_words(const char* hex, uint64_t w[4]) {
+  for (int i = 0; i < 4; ++i) {
+    uint64_t x = 0;
+    for (int j = 0; j < 16; ++j) {
+      const char ch = hex[16 * i + j];
+      const int d = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : -1;
+      if (d < 0) return false;
+      x = x << 4 | (uint64_t)d;
+    }
+    w[i] = x;
+  }
+  return true;
+}
+
+// The block every rank returns: *tmpl with the winning counter's nonce and the
+// finder's digest as 64 hex chars + NUL (pow_mine's strcpy semantics,
+// node.cpp:318: bytes 65..255 keep the template's).
+void winner_block(const pow_block* tmpl, uint64_t ctr, const uint64_t w[4], pow_block* out) {
+  static const char hexd[] = "0123456789abcdef";
+  *out = *tmpl;
+  pow_nonce_from_counter(ctr, out->nonce);
+  for (int i = 0; i < 64; ++i) out->block_hash[i] = hexd[(w[i / 16] >> (4 * (15 - i % 16))) & 15];
+  out->block_hash[64] = 0;
 }
 
 // Rounds of a collective search (both modes): every rank mines its static
@@ -375,14 +390,14 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
     uint64_t v[3] = {UINT64_MAX, 1, 1};
     int local_rc = POW_OK;
     char local_err[512] = {0};
+    pow_block mine_blk;  // this rank's own solution of the round (local_rc == 1)
+    uint64_t c = UINT64_MAX;
     ++info.rounds;
     info.local_found = 0;
     if (k) {
-      pow_block tmp;
-      uint64_t c = 0;
       const uint64_t m0 = now_ns();
-      local_rc = any ? pow_mine_any(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, nullptr)
-                     : pow_mine(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &tmp, &c, nullptr);
+      local_rc = any ? pow_mine_any(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &mine_blk, &c, nullptr)
+                     : pow_mine(g->ctx, tmpl, s, k, diff_bits, cancel_word, epoch, &mine_blk, &c, nullptr);
       info.mine_end_ns = now_ns();
       info.mine_ms += (info.mine_end_ns - m0) * 1e-6;
       st.add(g->ctx);
@@ -425,9 +440,20 @@ int group_search(pow_group* g, const pow_block* tmpl, uint64_t ctr_start, uint64
       return local_rc < 0 ? pow_set_error(local_rc, local_err) : pow_set_error(POW_ECOMM, "a peer rank failed");
     if (v[1] == 0) return 0;  // cancelled on some rank
     if (v[0] != UINT64_MAX) {
-      pow_board_bind(g->ctx, nullptr, 0, 0);
-      if (int rc = winner_block(g, tmpl, v[0], out, st)) return rc;
-      pow_ctx_set_stats(g->ctx, st.s);
+      // The winner: the rank whose own solution it is contributes its digest
+      // (4 words + a presence word; zeros elsewhere) to one all-reduce(max), and
+      // every rank writes the same block from it.  No rank re-hashes the winner,
+      // so no rank can fail alone after the ranks agreed (round 5 re-hashed it
+      // with a one-counter launch on every rank, whose failure on one rank left
+      // that rank with an error and the others with the block).
+      uint64_t w[5] = {0, 0, 0, 0, 0};
+      if (local_rc == 1 && c == v[0] && digest_words(mine_blk.block_hash, w)) w[4] = 1;
+      const uint64_t a1 = now_ns();
+      const int drc = group_allreduce(g, w, 5, POW_REDUCE_MAX);
+      info.allreduce_ms += (now_ns() - a1) * 1e-6;
+      if (drc) return drc;
+      if (w[4] != 1) return pow_set_error(POW_ECOMM, "the winner's digest did not arrive");
+      winner_block(tmpl, v[0], w, out);
       if (found_ctr) *found_ctr = v[0];
       return 1;
     }
