@@ -204,3 +204,34 @@ def test_private_lead_termination_race_reproduced(tmp_path):
         for r in range(4):
             assert f"[{r}] Perdí la carrera por varios contra" in out, (r, out[-3000:])
             assert f"[{r}]: find = 2 | received_blockchain_checks = 1" in out, (r, out[-3000:])
+
+
+def test_node_reports_placement(tmp_path):
+    """Every pow_node rank says which GPU it mines on: one `pow_node device`
+    line with the HIP device, the PCI address and the launcher variable that
+    chose it (VERDICT r05).  Under MPICH's mpiexec that is MPI_LOCALRANKID;
+    without it the node falls back to PMI_RANK (the global rank: the same on
+    one node).  MPICH cannot run a rank without PMI_RANK, so the no-variable
+    warning is covered by the CPU test of bench.node_placement."""
+    import subprocess
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from mpi_blockchain_amd.build import build_node
+    from mpi_blockchain_amd.node import MPIEXEC, mpi_env
+
+    node = build_node()
+    strip = ["env", "-u", "MPI_LOCALRANKID", "-u", "OMPI_COMM_WORLD_LOCAL_RANK", "-u", "LOCAL_RANK"]
+    for name, prefix, want in (("launcher", [], "MPI_LOCALRANKID"), ("pmi_rank", strip, "PMI_RANK")):
+        d = tmp_path / name
+        d.mkdir()
+        p = subprocess.run(["timeout", "-k", "10", "120", MPIEXEC, "-np", "2", *prefix, node, "--difficulty", "9"],
+                           cwd=d, env=mpi_env(), capture_output=True, text=True)
+        assert p.returncode == 0, (name, p.stdout[-2000:], p.stderr[-2000:])
+        pl = bench.node_placement(p.stdout + p.stderr, 2, rehearsal=True)
+        assert pl["ok"] and pl["all_ranks_reported"] and pl["no_local_rank_warnings"] == [], (name, pl)
+        assert [x["rank"] for x in pl["devices"]] == [0, 1] and [x["local_rank"] for x in pl["devices"]] == [0, 1], pl
+        assert [x["local_rank_from"] for x in pl["devices"]] == [want] * 2, (name, pl)
+        assert all(re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-9a-f]", x["pci"], re.I)
+                   for x in pl["devices"]), pl
