@@ -831,7 +831,7 @@ def valu_peaks(miner, device: int, cu_count: int) -> dict:
     out = {}
     for name, kind in (("full_rate", POW_VALU_FULL), ("half_rate", POW_VALU_HALF), ("sha_round", POW_VALU_MIX)):
         r = ValuResult()
-        if miner.L.pow_valu_rate(device, kind, ctypes.byref(r)) == 0:
+        if miner.L.pow_valu_rate_ctx(miner.ctx, kind, ctypes.byref(r)) == 0:  # on the miner's stream: no extra queue
             out[f"microbench_{name}"] = {"tops": round(r.lane_ops_per_s / 1e12, 2),
                                          "clock_ghz": round(r.clock_hz / 1e9, 4),
                                          "cycles_per_instr": round(r.cycles_per_instr, 3)}

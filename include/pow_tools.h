@@ -26,6 +26,11 @@ typedef struct pow_valu_result {
  * SIMD of 8 independent dependency chains per lane in the given mix.
  * Returns 0 or a POW_E* code. */
 int pow_valu_rate(int device, int kind, pow_valu_result* res);
+/* The same on a context's stream: the process holds no hardware queue more
+ * (HIP keeps a stream's queue after the stream is destroyed, so
+ * pow_valu_rate's own stream adds one for the process's lifetime). */
+struct pow_ctx;
+int pow_valu_rate_ctx(struct pow_ctx* ctx, int kind, pow_valu_result* res);
 
 /* pow_valu_rate(device, POW_VALU_MIX): lane-ops/s and kernel time. */
 int pow_valu_peak(int device, double* lane_ops_per_s, double* kernel_ms);

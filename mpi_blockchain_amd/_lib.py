@@ -159,6 +159,7 @@ def load(test_hooks: bool = False) -> ctypes.CDLL:
         "pow_valu_peak": ([ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
                           ctypes.c_int),
         "pow_valu_rate": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ValuResult)], ctypes.c_int),
+        "pow_valu_rate_ctx": ([ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ValuResult)], ctypes.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -172,7 +173,7 @@ EXPORTS = ("pow_device_count", "pow_init", "pow_warmup", "pow_destroy", "pow_las
            "pow_device_info", "pow_device_pci_bus_id",
            "pow_nonce_from_counter", "pow_block_to_bytes", "pow_solves_problem", "pow_hash_blocks",
            "pow_hash_block", "pow_mine", "pow_mine_any", "pow_cancel", "pow_sweep", "pow_sweep_device", "pow_dev_alloc", "pow_dev_free",
-           "pow_dev_read", "pow_valu_peak", "pow_valu_rate", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
+           "pow_dev_read", "pow_valu_peak", "pow_valu_rate", "pow_valu_rate_ctx", "pow_group_partition", "pow_group_unique_id", "pow_group_init",
            "pow_group_init_within",
            "pow_group_init_custom", "pow_group_destroy", "pow_group_info", "pow_group_rccl_path", "pow_group_last_search",
            "pow_group_allreduce_u64", "pow_group_mine", "pow_group_mine_any",

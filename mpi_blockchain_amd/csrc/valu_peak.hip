@@ -24,6 +24,7 @@
 
 #include "../../include/pow_gpu.h"
 #include "../../include/pow_tools.h"
+#include "pow_template.h"
 #include "sha256_dev.h"
 
 // iterations: ~2-3 ms per stream, long enough for a steady clock reading
@@ -88,7 +89,13 @@ __global__ __launch_bounds__(256) void valu_rate_kernel(uint32_t seed, uint32_t*
 // and branch are scalar): checked against the disassembly in tests/test_build.py.
 static int instrs_per_iter(int kind) { return kind == POW_VALU_MIX ? 8 * 14 : 16; }
 
-extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
+// The measurement on stream `st` of `device`.  Every launch, event and copy
+// goes on that stream (never HIP's null stream: DESIGN.md §7, "Queue
+// pressure"), and every wait is bounded (30 s).  *drained = false: a launch
+// may still be running after a wait ran out; its events and buffers are then
+// leaked rather than freed under it.
+static int valu_rate_on(int device, hipStream_t st, int kind, pow_valu_result* res, bool* drained) {
+  *drained = true;
   if (!res || kind < POW_VALU_MIX || kind > POW_VALU_HALF) return POW_EINVAL;
   if (hipSetDevice(device) != hipSuccess) return POW_ENODEV;
   hipDeviceProp_t prop;
@@ -96,13 +103,6 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   int rt_khz = 100000;
   (void)hipDeviceGetAttribute(&rt_khz, hipDeviceAttributeWallClockRate, device);
   const unsigned grid = (unsigned)prop.multiProcessorCount * 8u;  // 32 waves per CU
-  // Every launch, event and copy on a stream of this call's own (never HIP's
-  // null stream, which would give the calling process one hardware queue more
-  // for as long as it lives: DESIGN.md §7, "Queue pressure"), and every wait
-  // bounded (30 s).  A wait that runs out leaks the buffers instead of freeing
-  // them under a kernel that may still write them.
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return POW_EHIP;
   uint32_t* out = nullptr;
   unsigned long long* stamps = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -112,7 +112,6 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
     if (e1) (void)hipEventDestroy(e1);
     (void)hipFree(out);
     (void)hipFree(stamps);
-    (void)hipStreamDestroy(st);
     return POW_EHIP;
   }
   auto wait = [&](hipEvent_t ev) {  // bounded: POW_OK, POW_EHIP on an error or after 30 s
@@ -128,7 +127,6 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   double best_clock = 0;
   std::vector<unsigned long long> h(2 * (size_t)grid);
   int rc = POW_OK;
-  bool drained = true;
   for (int rep = 0; rep < 4 && rc == POW_OK; ++rep) {  // rep 0 warms up clocks
     (void)hipEventRecord(e0, st);
     if (kind == POW_VALU_MIX)
@@ -140,11 +138,11 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
     (void)hipEventRecord(e1, st);
     if (hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess) {
       rc = POW_EHIP;
-      drained = wait(e1) == POW_OK;
+      *drained = wait(e1) == POW_OK;
       break;
     }
     if ((rc = wait(e1)) != POW_OK || (rc = hipStreamSynchronize(st) == hipSuccess ? POW_OK : POW_EHIP) != POW_OK) {
-      drained = hipEventQuery(e1) == hipSuccess;
+      *drained = hipEventQuery(e1) == hipSuccess;
       break;
     }
     float ms = 0;
@@ -160,12 +158,11 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
       best_clock = clk.empty() ? 0 : clk[clk.size() / 2];
     }
   }
-  if (!drained) return rc;  // a launch may still be running: keep its stream, events and buffers
+  if (!*drained) return rc;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipFree(out);
   (void)hipFree(stamps);
-  (void)hipStreamDestroy(st);
   if (rc != POW_OK) return rc;
   const double wave_instr = (double)grid * 4.0 * VP_ITERS(kind) * instrs_per_iter(kind);
   res->lane_ops_per_s = wave_instr * 64.0 / (best * 1e-3);
@@ -174,6 +171,29 @@ extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
   const double simds = (double)prop.multiProcessorCount * 4.0;
   res->cycles_per_instr = best_clock > 0 ? simds * best_clock * (best * 1e-3) / wave_instr : 0;
   return POW_OK;
+}
+
+// A stream of this call's own.  HIP does not give the hardware queue behind
+// it back when the stream is destroyed (hsa_queue_destroy is never called:
+// tools/queue_trace.sh), so a process that has a pow_ctx should use
+// pow_valu_rate_ctx instead.
+extern "C" int pow_valu_rate(int device, int kind, pow_valu_result* res) {
+  if (!res || kind < POW_VALU_MIX || kind > POW_VALU_HALF) return POW_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return POW_ENODEV;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return POW_EHIP;
+  bool drained = true;
+  const int rc = valu_rate_on(device, st, kind, res, &drained);
+  if (drained) (void)hipStreamDestroy(st);
+  return rc;
+}
+
+// On the context's own stream: no hardware queue beyond the one the context
+// already holds.
+extern "C" int pow_valu_rate_ctx(pow_ctx* ctx, int kind, pow_valu_result* res) {
+  if (!ctx) return POW_EINVAL;
+  bool drained = true;
+  return valu_rate_on(pow_ctx_device(ctx), (hipStream_t)pow_ctx_stream(ctx), kind, res, &drained);
 }
 
 extern "C" int pow_valu_peak(int device, double* lane_ops_per_s, double* kernel_ms) {

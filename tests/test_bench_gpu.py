@@ -69,6 +69,15 @@ def test_valu_microbench_ceilings():
     assert out[POW_VALU_FULL].cycles_per_instr < out[POW_VALU_MIX].cycles_per_instr < \
         out[POW_VALU_HALF].cycles_per_instr
     assert L.pow_valu_rate(0, 7, ctypes.byref(ValuResult())) < 0
+    # the same measurement on a context's stream (bench.py's form: no extra hardware queue)
+    from mpi_blockchain_amd.miner import GpuMiner
+
+    with GpuMiner(0) as m:
+        r = ValuResult()
+        assert m.L.pow_valu_rate_ctx(m.ctx, POW_VALU_FULL, ctypes.byref(r)) == 0
+        assert 0.8 < r.lane_ops_per_s / out[POW_VALU_FULL].lane_ops_per_s < 1.25, r.lane_ops_per_s
+        assert 1.9 < r.cycles_per_instr < 2.6
+        assert m.L.pow_valu_rate_ctx(None, POW_VALU_FULL, ctypes.byref(r)) < 0
 
 
 def run_rehearsal(n: int, transport: str = "gloo") -> dict:
