@@ -941,15 +941,33 @@ def native_group_error(group, group_err: str | None, world: int, rehearsal: bool
     return None
 
 
-def rank_timing(rank: int, kernel_ms: list, allreduce_ms: list, own_wall_s: float, steps: int) -> dict:
+def rank_timing(rank: int, kernel_ms: list, allreduce_ms: list, own_wall_s: float, steps: int,
+                clock_ghz: float | None = None) -> dict:
     """One rank's timed steps: mean HIP-event kernel ms per step, mean wall ms
     in the step's two all-reduces (pow_group_allreduce_u64; waiting for slower
-    peers included), and the rank's own wall ms per step before the closing
-    barrier."""
+    peers included), the rank's own wall ms per step before the closing
+    barrier, and the shader clock its GPU held under load right after them
+    (clock_ghz: pow_valu_rate_ctx's K1-mix probe, run by every rank at once)."""
     return {"rank": rank,
             "kernel_ms": round(statistics.mean(kernel_ms), 3) if kernel_ms else None,
             "allreduce_ms": round(statistics.mean(allreduce_ms), 3) if allreduce_ms else 0.0,
-            "step_ms": round(1e3 * own_wall_s / max(1, steps), 3)}
+            "step_ms": round(1e3 * own_wall_s / max(1, steps), 3),
+            "clock_ghz": round(clock_ghz, 4) if clock_ghz else None}
+
+
+def loaded_clock_ghz(miner) -> float | None:
+    """The shader clock this rank's GPU holds under the K1 instruction mix,
+    measured on the miner's stream (pow_valu_rate_ctx, POW_VALU_MIX; ~0.1 s).
+    Every rank runs it at the same moment, so at N > 1 it is the clock under
+    the whole node's load: a GPU whose clock droops shows here."""
+    import ctypes
+
+    from mpi_blockchain_amd._lib import POW_VALU_MIX, ValuResult
+
+    r = ValuResult()
+    if miner.L.pow_valu_rate_ctx(miner.ctx, POW_VALU_MIX, ctypes.byref(r)) != 0 or r.clock_hz <= 0:
+        return None
+    return r.clock_hz / 1e9
 
 
 def timing_block(ranks: list[dict], ms_per_step: float) -> dict:
@@ -965,10 +983,12 @@ def timing_block(ranks: list[dict], ms_per_step: float) -> dict:
             "per_rank_other_ms": [round(ms_per_step - (r.get("kernel_ms") or 0) - (r.get("allreduce_ms") or 0), 3)
                                   for r in ranks],
             "imbalance": round(max(ks) / min(ks), 4) if ks and min(ks) > 0 else None,
+            "per_rank_clock_ghz": [r.get("clock_ghz") for r in ranks],
             "slowest_kernel_rank": max(ranks, key=lambda r: r.get("kernel_ms") or 0)["rank"] if ranks else None,
             "note": "kernel = HIP-event time of the step's sweep; allreduce = wall time of its two "
                     "pow_group_allreduce_u64 calls (min, sum), waiting for peers included; other = ms_per_step "
-                    "minus both"}
+                    "minus both; clock = the shader clock each GPU held under the K1 mix, all ranks at once, "
+                    "right after the timed steps"}
 
 
 def main():
@@ -1162,7 +1182,9 @@ def run_rank(args, ph: RankPhases, world: int, rank: int, local: int) -> None:
     ph.enter("parity", 120)
     n_loc = local_last[0][0]
     local_last[0] = (*local_last[0], list_fingerprint(buf, n_loc) if d == 9 and n_loc <= cap else None)
-    my_timing = rank_timing(rank, kernel_ms, allreduce_ms, el_own, args.steps)
+    if dist is not None:
+        dist.barrier()  # every GPU loaded at once for the clock probe
+    my_timing = rank_timing(rank, kernel_ms, allreduce_ms, el_own, args.steps, loaded_clock_ghz(miner))
     per_rank = [(local_last[0], my_timing)]
     if dist is not None:
         per_rank = [None] * world

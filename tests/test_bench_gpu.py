@@ -130,6 +130,7 @@ def run_rehearsal(n: int, transport: str = "gloo") -> dict:
         assert k > 0 and a > 0 and k + a <= 1.05 * st + 1.0, tm
         assert max(st, k + a) <= 1.05 * d["ms_per_step"] + 1.0, tm  # nobody's step exceeds the job's
     assert tm["imbalance"] >= 1.0 and d["imbalance"] == tm["imbalance"], tm
+    assert len(tm["per_rank_clock_ghz"]) == n and all(1.0 < c < 2.6 for c in tm["per_rank_clock_ghz"]), tm
     # the stop board: open and bound on every rank, and peers stopped by it (not at the round's end)
     bd = gs["board"]
     assert [r["rank"] for r in bd["per_rank"]] == list(range(n)), bd

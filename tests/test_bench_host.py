@@ -301,7 +301,9 @@ def test_timing_block():
     """Per-rank attribution of the N > 1 step: kernel, all-reduce, own step,
     what is left of the job's step, and the kernel imbalance (max / min)."""
     ranks = [bench.rank_timing(r, [470.0 + r, 470.0 + r], [0.2, 0.3], 0.4715 * 2, 2) for r in range(4)]
-    assert ranks[3] == {"rank": 3, "kernel_ms": 473.0, "allreduce_ms": 0.25, "step_ms": 471.5}
+    assert ranks[3] == {"rank": 3, "kernel_ms": 473.0, "allreduce_ms": 0.25, "step_ms": 471.5, "clock_ghz": None}
+    with_clk = bench.rank_timing(0, [470.0], [0.2], 0.47, 1, 2.38123)
+    assert with_clk["clock_ghz"] == 2.3812 and bench.timing_block([with_clk], 470.5)["per_rank_clock_ghz"] == [2.3812]
     t = bench.timing_block(ranks, 474.0)
     assert t["per_rank_kernel_ms"] == [470.0, 471.0, 472.0, 473.0]
     assert t["allreduce_ms_per_step"] == [0.25] * 4 and t["slowest_kernel_rank"] == 3
